@@ -1,0 +1,10 @@
+// Aggregates the per-family op registrations into the extension module.
+#include "ops_decl.h"
+
+namespace sdx_bind {
+void register_supcon(pybind11::module& m);
+
+void register_ops(pybind11::module& m) {
+  register_supcon(m);
+}
+}  // namespace sdx_bind

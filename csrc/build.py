@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""In-tree build of the gfx950 extension ``simclr_pytorch_distributed_amd/_C.so``.
+
+Design (no hipify, no setuptools CUDAExtension): the HIP kernels in ``csrc/kernels``
+are plain HIP (no torch headers) compiled by ``hipcc --offload-arch=gfx950``; the
+binding TUs in ``csrc/bindings`` include torch headers and are compiled host-only.
+Objects are cached under ``build/obj`` keyed on source mtime, included-header mtimes
+and the flag string, and compiled in parallel. The final shared object is written
+inside the package so it travels to the GPU box with the repo snapshot.
+
+Usage: ``python csrc/build.py [--force] [--jobs N] [--debug]``
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "simclr_pytorch_distributed_amd")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+OUT = os.path.join(PKG, "_C.so")
+ARCH = os.environ.get("SDX_OFFLOAD_ARCH", "gfx950")
+
+
+def _torch_paths():
+    import torch
+    import torch.utils.cpp_extension as ce
+    return ce.include_paths(), ce.library_paths(), int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _headers_mtime():
+    m = 0.0
+    for d in (os.path.join(CSRC, "include"),):
+        for f in os.listdir(d):
+            m = max(m, os.path.getmtime(os.path.join(d, f)))
+    return m
+
+
+def _sources():
+    kern = sorted(os.path.join(CSRC, "kernels", f) for f in os.listdir(os.path.join(CSRC, "kernels"))
+                  if f.endswith(".hip"))
+    bind = sorted(os.path.join(CSRC, "bindings", f) for f in os.listdir(os.path.join(CSRC, "bindings"))
+                  if f.endswith(".cpp"))
+    return kern, bind
+
+
+def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    inc_torch, lib_torch, abi = _torch_paths()
+    hipcc = _hipcc()
+    py_inc = sysconfig.get_paths()["include"]
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    common = ["-std=c++17", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-Wno-unused-result",
+              "-Wno-deprecated-declarations"]
+    kflags = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+              "-ffp-contract=fast"] + opt + common
+    bflags = [os.environ.get("CXX", "g++"), "-O2", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+              "-I/opt/rocm/include",
+              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+              "-DTORCH_EXTENSION_NAME=_C", f"-I{py_inc}"] + [f"-I{p}" for p in inc_torch] + common
+    hdr_m = _headers_mtime()
+    kern, bind = _sources()
+
+    def job(src, flags):
+        key = hashlib.sha1((" ".join(flags) + src).encode()).hexdigest()[:10]
+        obj = os.path.join(OBJ_DIR, os.path.basename(src) + f".{key}.o")
+        if (not force and os.path.exists(obj)
+                and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_m)):
+            return obj, False
+        cmd = flags + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+        return obj, True
+
+    tasks = [(s, kflags) for s in kern] + [(s, bflags) for s in bind]
+    n = jobs or min(8, os.cpu_count() or 4)
+    with ThreadPoolExecutor(max_workers=n) as ex:
+        results = list(ex.map(lambda t: job(*t), tasks))
+    objs = [o for o, _ in results]
+    rebuilt = any(r for _, r in results)
+    if rebuilt or force or not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs):
+        libs = []
+        for p in lib_torch:
+            libs += [f"-L{p}", f"-Wl,-rpath,{p}"]
+        libs += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
+        tmp = OUT + ".tmp"
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + libs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, OUT)
+    return OUT
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    out = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose)
+    print(out)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,59 @@
+// Common device helpers for the gfx950 (CDNA4, MI355X) kernels of this framework.
+// Everything here is written for wave64 and the CDNA4 MFMA register maps; there is
+// no portability layer and no CUDA-compatible path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace sdx {
+
+constexpr int kWave = 64;   // CDNA wavefront width (never 32)
+constexpr int kNumXcd = 8;  // MI355X: 8 XCDs x 32 CUs
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (4 VGPR)
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16;  // 32x32 accumulator
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// Round-to-nearest-even float -> bf16 via the hardware conversion (keeps NaN a NaN).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md T1): consecutive logical
+// tiles land on the same XCD so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg < kNumXcd) return bid;
+  const int q = nwg / kNumXcd, r = nwg % kNumXcd;
+  const int xcd = bid % kNumXcd, idx = bid / kNumXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace sdx
+
+#define SDX_LAUNCH_CHECK() \
+  do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return e__; } while (0)

@@ -1,0 +1,12 @@
+// Registration hooks of the per-family binding translation units. Splitting the
+// bindings keeps each torch-header-heavy TU small so incremental rebuilds stay fast.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <torch/extension.h>
+
+namespace sdx_bind {
+hipStream_t cur_stream();
+void check_hip(hipError_t e, const char* what);
+
+void register_ops(pybind11::module& m);
+}  // namespace sdx_bind

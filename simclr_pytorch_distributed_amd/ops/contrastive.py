@@ -1,0 +1,52 @@
+"""Autograd binding of the fused contrastive-loss kernels (csrc/kernels/supcon.hip).
+
+``supcon_rows_loss(A, C, self_idx, akey, ckey, τ, τ_base, scale)`` returns
+``scale * Σ_i ℓ_i`` for the anchor rows ``A`` (rows of ``C``, the L2-normalised
+contrast matrix). Forward: one split tile kernel + one finalize kernel; backward: two
+tile kernels (dA, dC). The upstream gradient stays on device (no host sync), so the op
+is hipGraph-capturable. Oracle: ``losses.supcon.supcon_rows_reference``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+
+_SUPPORTED_D = (64, 128, 256)
+
+
+def supported(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dim() == 2 and t.shape[1] in _SUPPORTED_D and _ext.available()
+
+
+class _SupConRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, C, self_idx, akey, ckey, temperature, base_temperature, scale):
+        m = _ext.require()
+        A32 = A.float().contiguous()
+        C32 = C.float().contiguous()
+        si = self_idx.to(torch.int32).contiguous()
+        ak = akey.to(torch.int32).contiguous()
+        ck = ckey.to(torch.int32).contiguous()
+        ratio = temperature / base_temperature
+        loss, lse, invcnt, row_loss = m.supcon_fwd(A32, C32, si, ak, ck, 1.0 / temperature, ratio, scale)
+        ctx.save_for_backward(A32, C32, si, ak, ck, lse, invcnt)
+        ctx.w = scale * ratio / temperature
+        ctx.inv_temp = 1.0 / temperature
+        ctx.dtypes = (A.dtype, C.dtype)
+        ctx.mark_non_differentiable(row_loss)
+        return loss.view(()), row_loss
+
+    @staticmethod
+    def backward(ctx, g, _g_rows):
+        m = _ext.require()
+        A32, C32, si, ak, ck, lse, invcnt = ctx.saved_tensors
+        gl = g.float().reshape(1).contiguous()
+        dA, dC = m.supcon_bwd(A32, C32, si, ak, ck, lse, invcnt, gl, ctx.inv_temp, ctx.w)
+        return dA.to(ctx.dtypes[0]), dC.to(ctx.dtypes[1]), None, None, None, None, None, None
+
+
+def supcon_rows_loss(A, C, self_idx, akey, ckey, temperature, base_temperature, scale, return_rows=False):
+    loss, rows = _SupConRows.apply(A, C, self_idx, akey, ckey, float(temperature), float(base_temperature),
+                                   float(scale))
+    return (loss, rows) if return_rows else loss

@@ -1,0 +1,127 @@
+"""Process-group bootstrap and differentiable collectives.
+
+Bootstrap (replaces main_supcon.py:357-364): ranks come from the launcher environment
+(``RANK``/``LOCAL_RANK``/``WORLD_SIZE``), rendezvous is ``env://`` against
+``MASTER_ADDR``/``MASTER_PORT``, the backend is RCCL (``"nccl"``) on GPUs and gloo on
+CPU. A collective timeout is always set so a dead peer produces an error
+instead of a hang.
+
+Differentiable collectives:
+
+* :func:`all_gather_with_grad` — forward all-gather of a per-rank block; backward is a
+  reduce-scatter (sum) of the gathered gradient back to its owners. This is what makes
+  the cross-GPU negatives of the contrastive loss (reference main_supcon.py:268-281,
+  which only supported exactly 2 ranks and dropped the gradients of gathered copies)
+  exact for any world size.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_dist() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_dist() else 0
+
+
+def backend() -> Optional[str]:
+    return dist.get_backend() if is_dist() else None
+
+
+def init_distributed(backend_name: str = "auto", timeout_s: float = 600.0, device: Optional[torch.device] = None):
+    """Initialise the default process group if the launcher started >1 rank.
+
+    Returns (rank, local_rank, world_size, device).
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rnk = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available()
+    if device is None:
+        device = torch.device(f"cuda:{local}") if use_cuda else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    if world > 1 and not is_dist():
+        if backend_name == "auto":
+            backend_name = "nccl" if device.type == "cuda" else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=backend_name, init_method="env://", world_size=world, rank=rnk,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if backend_name == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return rnk, local, world, device
+
+
+def barrier():
+    if is_dist():
+        if backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def _supports_reduce_scatter() -> bool:
+    return backend() == "nccl"
+
+
+def all_gather_tensor(x: torch.Tensor) -> torch.Tensor:
+    """Gather equal-sized blocks along dim 0 (no autograd)."""
+    w = world_size()
+    if w == 1:
+        return x
+    x = x.contiguous()
+    out = torch.empty((w * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x)
+    return out
+
+
+def reduce_scatter_tensor(x: torch.Tensor) -> torch.Tensor:
+    """Sum over ranks, then return this rank's dim-0 block (no autograd)."""
+    w = world_size()
+    if w == 1:
+        return x
+    x = x.contiguous()
+    n = x.shape[0] // w
+    if _supports_reduce_scatter():
+        out = torch.empty((n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, x)
+        return out
+    y = x.clone()
+    dist.all_reduce(y)
+    r = rank()
+    return y[r * n:(r + 1) * n].contiguous()
+
+
+class _AllGatherGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return all_gather_tensor(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return reduce_scatter_tensor(g)
+
+
+def all_gather_with_grad(x: torch.Tensor) -> torch.Tensor:
+    if world_size() == 1:
+        return x
+    return _AllGatherGrad.apply(x)
+
+
+def all_reduce_sum_(x: torch.Tensor) -> torch.Tensor:
+    if world_size() > 1:
+        dist.all_reduce(x)
+    return x
