@@ -30,8 +30,9 @@ def supcon_rows_reference(A: torch.Tensor, C: torch.Tensor, self_idx: torch.Tens
                           akey: torch.Tensor, ckey: torch.Tensor, temperature: float,
                           base_temperature: float) -> torch.Tensor:
     """Per-anchor loss ℓ_i (pure torch, fp32; CPU path and kernel oracle)."""
-    A = A.float()
-    C = C.float()
+    dt = torch.promote_types(torch.promote_types(A.dtype, C.dtype), torch.float32)
+    A = A.to(dt)
+    C = C.to(dt)
     logits = A @ C.t() / temperature
     n = C.shape[0]
     cols = torch.arange(n, device=C.device)
