@@ -1,0 +1,318 @@
+// Bindings for the implicit-GEMM convolution (igemm.hip) and BatchNorm (bn.hip) kernels.
+// Host-side shape/dtype/layout checks run before every launch.
+#include "ops_decl.h"
+#include "launchers.h"
+
+namespace sdx_bind {
+namespace {
+
+using OptT = c10::optional<torch::Tensor>;
+
+void check_bf16_nhwc(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(), name, " must be a contiguous 4-D (NHWC) tensor");
+  TORCH_CHECK(t.size(3) % 8 == 0, name, ": channel count must be a multiple of 8");
+  TORCH_CHECK(t.numel() < (1LL << 31), name, " too large for 32-bit GEMM indexing");
+}
+
+int auto_cfg(int64_t M, int64_t Ncol) {
+  if (Ncol <= 64) return 1;          // 256 x 64
+  if (M <= 64) return 2;             // 64 x 256
+  return 0;                          // 128 x 128
+}
+
+std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
+                                    int64_t cfg) {
+  check_bf16_nhwc(x, "x");
+  check_bf16_nhwc(w, "w");
+  TORCH_CHECK(w.size(3) == x.size(3), "weight Cin != input C");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
+  ConvGeom g{};
+  g.N = x.size(0); g.H = x.size(1); g.W = x.size(2); g.C = x.size(3);
+  g.K = w.size(0); g.R = w.size(1); g.S = w.size(2);
+  g.stride = stride; g.pad = pad;
+  g.P = (g.H + 2 * pad - g.R) / stride + 1;
+  g.Q = (g.W + 2 * pad - g.S) / stride + 1;
+  TORCH_CHECK(g.P > 0 && g.Q > 0, "empty output");
+  TORCH_CHECK(g.K % 8 == 0, "Cout must be a multiple of 8");
+  c10::DeviceGuard dg(x.device());
+  const int64_t M = (int64_t)g.N * g.P * g.Q;
+  if (cfg < 0) cfg = auto_cfg(M, g.K);
+  auto y = torch::empty({g.N, g.P, g.Q, g.K}, x.options());
+  torch::Tensor slab;
+  float* sp = nullptr;
+  if (want_stats) {
+    const int64_t mt = (M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg);
+    slab = torch::empty({mt, 2, g.K}, x.options().dtype(at::kFloat));
+    sp = slab.data_ptr<float>();
+  } else {
+    slab = torch::empty({0}, x.options().dtype(at::kFloat));
+  }
+  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream()), "conv_fwd");
+  return {y, slab};
+}
+
+torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                         int64_t cfg) {
+  check_bf16_nhwc(dy, "dy");
+  check_bf16_nhwc(wt, "wt");
+  TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
+  ConvGeom g{};
+  g.N = dy.size(0); g.P = dy.size(1); g.Q = dy.size(2); g.K = dy.size(3);
+  g.C = wt.size(0); g.R = wt.size(1); g.S = wt.size(2);
+  g.H = H; g.W = W; g.stride = stride; g.pad = pad;
+  TORCH_CHECK((g.H + 2 * pad - g.R) / stride + 1 == g.P && (g.W + 2 * pad - g.S) / stride + 1 == g.Q,
+              "dgrad geometry mismatch");
+  TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
+  c10::DeviceGuard dg(dy.device());
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  if (cfg < 0) cfg = auto_cfg(M, g.C);
+  auto dx = torch::empty({g.N, g.H, g.W, g.C}, dy.options());
+  check_hip(launch_conv_dgrad(g, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)cfg, cur_stream()), "conv_dgrad");
+  return dx;
+}
+
+torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                         int64_t splits, int64_t cfg) {
+  check_bf16_nhwc(dy, "dy");
+  check_bf16_nhwc(x, "x");
+  TORCH_CHECK(dy.size(0) == x.size(0), "batch mismatch");
+  ConvGeom g{};
+  g.N = x.size(0); g.H = x.size(1); g.W = x.size(2); g.C = x.size(3);
+  g.P = dy.size(1); g.Q = dy.size(2); g.K = dy.size(3);
+  g.R = R; g.S = S; g.stride = stride; g.pad = pad;
+  TORCH_CHECK((g.H + 2 * pad - R) / stride + 1 == g.P && (g.W + 2 * pad - S) / stride + 1 == g.Q,
+              "wgrad geometry mismatch");
+  c10::DeviceGuard dg(x.device());
+  const int64_t M = g.K, Ncol = (int64_t)R * S * g.C, Kd = (int64_t)g.N * g.P * g.Q;
+  if (cfg < 0) cfg = (M <= 64) ? 2 : (Ncol <= 64 ? 1 : 0);
+  if (splits <= 0) {
+    const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
+                          ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
+    splits = std::max<int64_t>(1, 512 / tiles);
+    const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
+    splits = std::min(splits, max_splits);
+  }
+  auto dw = torch::zeros({g.K, R, S, g.C}, x.options().dtype(at::kFloat));
+  check_hip(launch_conv_wgrad(g, dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), (int)cfg, (int)splits,
+                              cur_stream()),
+            "conv_wgrad");
+  return dw;
+}
+
+void check_vec(const torch::Tensor& t, int64_t C, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, name,
+              " must be a contiguous float32 GPU vector of length C");
+}
+
+const float* opt_ptr(const OptT& t, int64_t C, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_vec(*t, C, name);
+  return t->data_ptr<float>();
+}
+
+torch::Tensor bn_stats_reduce(torch::Tensor slab) {
+  TORCH_CHECK(slab.is_cuda() && slab.scalar_type() == at::kFloat && slab.dim() == 3 && slab.size(1) == 2 &&
+                  slab.is_contiguous(),
+              "slab must be [rows, 2, C] float32");
+  c10::DeviceGuard dg(slab.device());
+  const int64_t C = slab.size(2);
+  auto out = torch::empty({2, C}, slab.options().dtype(at::kDouble));
+  check_hip(launch_bn_stats_reduce(slab.data_ptr<float>(), slab.size(0), C, out.data_ptr<double>(), cur_stream()),
+            "bn_stats_reduce");
+  return out;
+}
+
+std::vector<torch::Tensor> bn_finalize(torch::Tensor sums, double count, OptT gamma, OptT beta, double eps,
+                                       double momentum, bool update, OptT running_mean, OptT running_var) {
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.dim() == 2 && sums.size(0) == 2 &&
+                  sums.is_contiguous(),
+              "sums must be [2, C] float64");
+  const int64_t C = sums.size(1);
+  c10::DeviceGuard dg(sums.device());
+  const float* gp = opt_ptr(gamma, C, "gamma");
+  const float* bp = opt_ptr(beta, C, "beta");
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (update) {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "running stats required for update");
+    check_vec(*running_mean, C, "running_mean");
+    check_vec(*running_var, C, "running_var");
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  auto fo = sums.options().dtype(at::kFloat);
+  auto scale = torch::empty({C}, fo), shift = torch::empty({C}, fo);
+  auto mean = torch::empty({C}, fo), invstd = torch::empty({C}, fo);
+  check_hip(launch_bn_finalize(sums.data_ptr<double>(), C, count, gp, bp, (float)eps, (float)momentum, update ? 1 : 0,
+                               rm, rv, scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
+                               invstd.data_ptr<float>(), cur_stream()),
+            "bn_finalize");
+  return {scale, shift, mean, invstd};
+}
+
+std::vector<torch::Tensor> bn_eval_affine(OptT gamma, OptT beta, torch::Tensor rm, torch::Tensor rv, double eps) {
+  const int64_t C = rm.numel();
+  check_vec(rm, C, "running_mean");
+  check_vec(rv, C, "running_var");
+  c10::DeviceGuard dg(rm.device());
+  auto scale = torch::empty({C}, rm.options()), shift = torch::empty({C}, rm.options());
+  check_hip(launch_bn_eval_affine(C, opt_ptr(gamma, C, "gamma"), opt_ptr(beta, C, "beta"), rm.data_ptr<float>(),
+                                  rv.data_ptr<float>(), (float)eps, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                  cur_stream()),
+            "bn_eval_affine");
+  return {scale, shift};
+}
+
+torch::Tensor bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, OptT r, OptT scale2, OptT shift2,
+                       int64_t res_mode, bool relu) {
+  check_bf16_nhwc(y, "y");
+  const int64_t C = y.size(3);
+  check_vec(scale, C, "scale");
+  check_vec(shift, C, "shift");
+  const void* rp = nullptr;
+  const float *s2 = nullptr, *t2 = nullptr;
+  TORCH_CHECK(res_mode >= 0 && res_mode <= 2, "res_mode");
+  if (res_mode != 0) {
+    TORCH_CHECK(r.has_value(), "residual tensor required");
+    check_bf16_nhwc(*r, "residual");
+    TORCH_CHECK(r->sizes() == y.sizes(), "residual shape mismatch");
+    rp = r->data_ptr();
+    if (res_mode == 1) {
+      s2 = opt_ptr(scale2, C, "scale2");
+      t2 = opt_ptr(shift2, C, "shift2");
+      TORCH_CHECK(s2 && t2, "scale2/shift2 required for res_mode 1");
+    }
+  }
+  c10::DeviceGuard dg(y.device());
+  auto out = torch::empty_like(y);
+  check_hip(launch_bn_apply(y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, s2, t2, (int)res_mode,
+                            relu ? 1 : 0, out.data_ptr(), y.numel(), C, cur_stream()),
+            "bn_apply");
+  return out;
+}
+
+void check_bwd_C(int64_t C) {
+  TORCH_CHECK(C <= 2048 && (C & (C - 1)) == 0 && C >= 8, "bn backward supports power-of-two C in [8, 2048]");
+}
+
+torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb) {
+  check_bf16_nhwc(dout, "dout");
+  check_bf16_nhwc(ya, "ya");
+  const int64_t C = dout.size(3);
+  check_bwd_C(C);
+  TORCH_CHECK(ya.sizes() == dout.sizes(), "ya shape");
+  check_vec(ma, C, "mean_a");
+  const void* op = nullptr;
+  if (outv.has_value()) {
+    check_bf16_nhwc(*outv, "out");
+    TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
+    op = outv->data_ptr();
+  }
+  const void* ybp = nullptr;
+  const float* mbp = nullptr;
+  if (yb.has_value()) {
+    check_bf16_nhwc(*yb, "yb");
+    TORCH_CHECK(yb->sizes() == dout.sizes(), "yb shape");
+    TORCH_CHECK(mb.has_value(), "mean_b required");
+    check_vec(*mb, C, "mean_b");
+    ybp = yb->data_ptr();
+    mbp = mb->data_ptr<float>();
+  }
+  c10::DeviceGuard dg(dout.device());
+  auto sums = torch::empty({ybp ? 3 : 2, C}, dout.options().dtype(at::kDouble));
+  check_hip(launch_bn_bwd_reduce(dout.data_ptr(), op, ya.data_ptr(), ma.data_ptr<float>(), ybp, mbp, dout.numel(), C,
+                                 sums.data_ptr<double>(), cur_stream()),
+            "bn_bwd_reduce");
+  return sums;
+}
+
+std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_a, torch::Tensor mean_a,
+                                       torch::Tensor inv_a, OptT g_b, OptT mean_b, OptT inv_b) {
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.dim() == 2 && sums.is_contiguous(),
+              "sums must be [nsets+1, C] float64");
+  const int64_t C = sums.size(1);
+  const int nsets = (int)sums.size(0) - 1;
+  TORCH_CHECK(nsets == 1 || nsets == 2, "1 or 2 BN sets");
+  check_vec(mean_a, C, "mean_a");
+  check_vec(inv_a, C, "inv_a");
+  c10::DeviceGuard dg(sums.device());
+  auto fo = sums.options().dtype(at::kFloat);
+  auto coef_a = torch::empty({3, C}, fo);
+  auto dga = torch::empty({C}, fo), dba = torch::empty({C}, fo);
+  torch::Tensor coef_b, dgb, dbb;
+  const float *gbp = nullptr, *mbp = nullptr, *ibp = nullptr;
+  if (nsets == 2) {
+    coef_b = torch::empty({3, C}, fo);
+    dgb = torch::empty({C}, fo);
+    dbb = torch::empty({C}, fo);
+    gbp = opt_ptr(g_b, C, "g_b");
+    mbp = opt_ptr(mean_b, C, "mean_b");
+    ibp = opt_ptr(inv_b, C, "inv_b");
+    TORCH_CHECK(mbp && ibp, "mean_b/inv_b required");
+  } else {
+    coef_b = dgb = dbb = torch::empty({0}, fo);
+  }
+  check_hip(launch_bn_bwd_coef(sums.data_ptr<double>(), nsets, C, count, opt_ptr(g_a, C, "g_a"),
+                               mean_a.data_ptr<float>(), inv_a.data_ptr<float>(), gbp, mbp, ibp,
+                               coef_a.data_ptr<float>(), nsets == 2 ? coef_b.data_ptr<float>() : nullptr,
+                               dga.data_ptr<float>(), dba.data_ptr<float>(),
+                               nsets == 2 ? dgb.data_ptr<float>() : nullptr,
+                               nsets == 2 ? dbb.data_ptr<float>() : nullptr, cur_stream()),
+            "bn_bwd_coef");
+  return {coef_a, coef_b, dga, dba, dgb, dbb};
+}
+
+std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ca, OptT yb,
+                                        OptT cb, bool want_dz) {
+  check_bf16_nhwc(dout, "dout");
+  check_bf16_nhwc(ya, "ya");
+  const int64_t C = dout.size(3);
+  TORCH_CHECK(ya.sizes() == dout.sizes(), "ya shape");
+  TORCH_CHECK(ca.is_cuda() && ca.scalar_type() == at::kFloat && ca.numel() == 3 * C && ca.is_contiguous(), "coef_a");
+  const void* op = nullptr;
+  if (outv.has_value()) {
+    check_bf16_nhwc(*outv, "out");
+    TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
+    op = outv->data_ptr();
+  }
+  c10::DeviceGuard dg(dout.device());
+  auto dya = torch::empty_like(dout);
+  torch::Tensor dyb, dz;
+  const void* ybp = nullptr;
+  const float* cbp = nullptr;
+  if (yb.has_value()) {
+    check_bf16_nhwc(*yb, "yb");
+    TORCH_CHECK(yb->sizes() == dout.sizes(), "yb shape");
+    TORCH_CHECK(cb.has_value() && cb->numel() == 3 * C && cb->scalar_type() == at::kFloat, "coef_b");
+    ybp = yb->data_ptr();
+    cbp = cb->data_ptr<float>();
+    dyb = torch::empty_like(dout);
+  } else {
+    dyb = torch::empty({0}, dout.options());
+  }
+  dz = want_dz ? torch::empty_like(dout) : torch::empty({0}, dout.options());
+  check_hip(launch_bn_bwd_apply(dout.data_ptr(), op, ya.data_ptr(), ca.data_ptr<float>(), ybp, cbp, dya.data_ptr(),
+                                ybp ? dyb.data_ptr() : nullptr, want_dz ? dz.data_ptr() : nullptr, dout.numel(), C,
+                                cur_stream()),
+            "bn_bwd_apply");
+  return {dya, dyb, dz};
+}
+
+}  // namespace
+
+void register_conv_bn(pybind11::module& m) {
+  m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16) + BN stat slab");
+  m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv data gradient");
+  m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K)");
+  m.def("bn_stats_reduce", &bn_stats_reduce);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_eval_affine", &bn_eval_affine);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_coef", &bn_bwd_coef);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+}
+
+}  // namespace sdx_bind

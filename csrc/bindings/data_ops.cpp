@@ -1,0 +1,39 @@
+// Bindings for the GPU data-pipeline kernels (aug.hip).
+#include "ops_decl.h"
+#include "launchers.h"
+
+namespace sdx_bind {
+namespace {
+
+torch::Tensor gpu_augment(torch::Tensor data, torch::Tensor idx, int64_t S, int64_t n_views, int64_t seed,
+                          std::vector<double> mean, std::vector<double> std, double scale_lo, double scale_hi,
+                          double ratio_lo, double ratio_hi, double jitter_p, double bright, double contrast,
+                          double sat, double hue, double gray_p, bool do_crop, bool do_flip) {
+  TORCH_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 4 && data.size(3) == 3 &&
+                  data.is_contiguous(),
+              "data must be a contiguous uint8 [N,H,W,3] GPU tensor");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(),
+              "idx must be a contiguous int64 GPU vector");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "mean/std need 3 values");
+  TORCH_CHECK(S >= 1 && n_views >= 1 && idx.size(0) >= 1, "bad sizes");
+  c10::DeviceGuard dg(data.device());
+  const int64_t B = idx.size(0);
+  auto out = torch::empty({n_views * B, S, S, 8}, data.options().dtype(at::kBFloat16));
+  float m[3], sd[3];
+  for (int k = 0; k < 3; ++k) { m[k] = (float)mean[k]; sd[k] = (float)std[k]; }
+  check_hip(launch_gpu_augment(data.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), (int)B, (int)data.size(1),
+                               (int)data.size(2), (int)S, (int)n_views, (uint64_t)seed, m, sd, (float)scale_lo,
+                               (float)scale_hi, (float)ratio_lo, (float)ratio_hi, (float)jitter_p, (float)bright,
+                               (float)contrast, (float)sat, (float)hue, (float)gray_p, do_crop ? 1 : 0,
+                               do_flip ? 1 : 0, out.data_ptr(), cur_stream()),
+            "gpu_augment");
+  return out;
+}
+
+}  // namespace
+
+void register_data(pybind11::module& m) {
+  m.def("gpu_augment", &gpu_augment, "fused SimCLR augmentation -> NHWC bf16 (C padded to 8)");
+}
+
+}  // namespace sdx_bind

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace sdx {
 

@@ -19,3 +19,45 @@ hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, 
                              const int* c_key, const float* lse, const float* invcnt, int Na, int N, int D,
                              float inv_temp, float w, const float* gscale, float* dA, float* dC,
                              hipStream_t s);
+
+// ---- implicit-GEMM convolution (igemm.hip) ------------------------------------
+struct ConvGeom {
+  int N, H, W, C;   // input NHWC
+  int K;            // output channels
+  int R, S;         // filter
+  int P, Q;         // output spatial
+  int stride, pad;
+};
+int igemm_tile_m(int cfg);
+int igemm_tile_n(int cfg);
+hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
+                           hipStream_t s);
+hipError_t launch_conv_dgrad(const ConvGeom& g, const void* dy, const void* wt, void* dx, int cfg,
+                             hipStream_t s);
+hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* dw, int cfg, int splits,
+                             hipStream_t s);
+
+// ---- BatchNorm (bn.hip) ---------------------------------------------------------
+hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s);
+hipError_t launch_bn_finalize(const double* sums, int C, double count, const float* gamma, const float* beta,
+                              float eps, float momentum, int update_running, float* running_mean, float* running_var,
+                              float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
+hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                                 float eps, float* scale, float* shift, hipStream_t s);
+hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, const void* r, const float* sc2,
+                           const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s);
+hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
+                                const float* mb, long numel, int C, double* sums, hipStream_t s);
+hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
+                              const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
+                              const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
+                              float* dgamma_b, float* dbeta_b, hipStream_t s);
+hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
+                               const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s);
+
+// ---- GPU augmentation (aug.hip) -------------------------------------------------
+hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, int H, int W, int S, int n_views,
+                              uint64_t seed, const float* mean, const float* std, float scale_lo, float scale_hi,
+                              float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
+                              float sat, float hue, float gray_p, int do_crop, int do_flip, void* out,
+                              hipStream_t s);

@@ -1,0 +1,367 @@
+// BatchNorm (training + eval) kernels for NHWC bf16 activations on gfx950.
+//
+// Forward statistics come from the convolution epilogue (igemm.hip: per-M-tile Σy, Σy²);
+// here they are reduced in fp64 (bn_stats_reduce), optionally all-reduced across ranks
+// by the caller (SyncBN: one fp64 all-reduce of [2][C] per layer), and turned into the
+// per-channel affine (bn_finalize, which also updates running_mean / running_var with
+// the unbiased variance, momentum 0.1 as torch BatchNorm2d). The affine is applied by
+// one fused elementwise pass together with the residual branch and the ReLU
+// (bn_apply: relu(bn(y) [+ bn'(y') | + x])) — reference: networks/resnet_big.py:57-67.
+//
+// Backward: bn_bwd_reduce recomputes dz = dout·[out>0] and accumulates Σdz and
+// Σdz·(y−μ) for up to two BNs sharing dz (residual branch + projection shortcut);
+// bn_bwd_coef folds those into per-channel (A, D, E) so that dy = A·dz + D·y + E, plus
+// dγ/dβ; bn_bwd_apply is one elementwise pass producing dy (and dz for an identity
+// shortcut). All elementwise kernels move 8 bf16 (16 B) per lane.
+#include "common.h"
+#include "launchers.h"
+
+using namespace sdx;
+
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+}
+
+// slab [rows][2][C] fp32 -> out [2][C] fp64 (out zeroed by the launcher)
+__global__ __launch_bounds__(256) void bn_stats_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                              double* __restrict__ out) {
+  __shared__ double red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);   // index into [2][C]
+  const int ty = threadIdx.x >> 6;
+  double acc = 0.0;
+  if (col < 2 * C) {
+    const int which = col / C, ch = col % C;
+    for (int r = blockIdx.y * 4 + ty; r < rows; r += gridDim.y * 4)
+      acc += (double)slab[((size_t)r * 2 + which) * C + ch];
+  }
+  red[ty][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (ty == 0 && col < 2 * C) {
+    const double s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(out + col, s);
+  }
+}
+
+// sums [2][C] fp64 (Σy, Σy²) over `count` rows -> scale/shift (+ mean/invstd for bwd),
+// running stats update (unbiased var) when `update_running`.
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                   float momentum, int update_running, float* __restrict__ running_mean,
+                                   float* __restrict__ running_var, float* __restrict__ scale,
+                                   float* __restrict__ shift, float* __restrict__ mean_out,
+                                   float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = sums[c] / count;
+  double var = sums[C + c] / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - (float)mean * g * invstd;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  if (update_running) {
+    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+// eval-mode affine from running statistics
+__global__ void bn_eval_affine_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                      const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                      float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  scale[c] = g * invstd;
+  shift[c] = (beta ? beta[c] : 0.f) - rm[c] * g * invstd;
+}
+
+// out = act(y*sc + sh [+ r*sc2 + sh2 | + r])     res_mode: 0 none, 1 bn'd residual, 2 raw residual
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ sc,
+                                                       const float* __restrict__ sh, const uint16_t* __restrict__ r,
+                                                       const float* __restrict__ sc2, const float* __restrict__ sh2,
+                                                       uint16_t* __restrict__ out, long n8, int C8) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n8; e += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(e % C8) * 8;
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[e], v);
+    const float4 s0 = reinterpret_cast<const float4*>(sc + c0)[0], s1 = reinterpret_cast<const float4*>(sc + c0)[1];
+    const float4 t0 = reinterpret_cast<const float4*>(sh + c0)[0], t1 = reinterpret_cast<const float4*>(sh + c0)[1];
+    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float tt[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = v[i] * ss[i] + tt[i];
+    if (RES != 0) {
+      float rv[8];
+      unpack8(reinterpret_cast<const uint4*>(r)[e], rv);
+      if (RES == 1) {
+        const float4 a0 = reinterpret_cast<const float4*>(sc2 + c0)[0], a1 = reinterpret_cast<const float4*>(sc2 + c0)[1];
+        const float4 b0 = reinterpret_cast<const float4*>(sh2 + c0)[0], b1 = reinterpret_cast<const float4*>(sh2 + c0)[1];
+        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += rv[i] * aa[i] + bb[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += rv[i];
+      }
+    }
+    if (RELU) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.f);
+    }
+    reinterpret_cast<uint4*>(out)[e] = pack8(v);
+  }
+}
+
+// Σdz, Σdz·(ya−μa) [, Σdz·(yb−μb)] with dz = dout·[out>0] (or dout when out == nullptr).
+// Threads keep a fixed 8-channel group (grid stride is a multiple of C/8).
+template <bool TWO>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dout,
+                                                            const uint16_t* __restrict__ outv,
+                                                            const uint16_t* __restrict__ ya, const float* __restrict__ ma,
+                                                            const uint16_t* __restrict__ yb, const float* __restrict__ mb,
+                                                            long n8, int C8, int C, double* __restrict__ sums) {
+  constexpr int NS = TWO ? 3 : 2;
+  __shared__ float red[NS][256][8];
+  const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const int grp = (int)(tid % C8);
+  const int c0 = grp * 8;
+  float mua[8], mub[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mua[i] = ma[c0 + i];
+    mub[i] = TWO ? mb[c0 + i] : 0.f;
+  }
+  float s0[8] = {0}, s1[8] = {0}, s2[8] = {0};
+  for (long e = tid; e < n8; e += stride) {
+    float d[8], a[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[e], d);
+    if (outv) {
+      float o[8];
+      unpack8(reinterpret_cast<const uint4*>(outv)[e], o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
+    }
+    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s0[i] += d[i];
+      s1[i] += d[i] * (a[i] - mua[i]);
+    }
+    if (TWO) {
+      float b[8];
+      unpack8(reinterpret_cast<const uint4*>(yb)[e], b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s2[i] += d[i] * (b[i] - mub[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[0][threadIdx.x][i] = s0[i];
+    red[1][threadIdx.x][i] = s1[i];
+    if (TWO) red[NS - 1][threadIdx.x][i] = s2[i];
+  }
+  __syncthreads();
+  // threads t and t + k*C8 (k>=1) within the block share the channel group
+  if ((int)threadIdx.x < C8 && C8 <= 256) {
+    double acc[NS][8];
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[q][i] = 0.0;
+    for (int t = threadIdx.x; t < 256; t += C8)
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[q][i] += red[q][t][i];
+    const int g0 = (int)((blockIdx.x * (long)blockDim.x + threadIdx.x) % C8) * 8;
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) atomicAdd(sums + (size_t)q * C + g0 + i, acc[q][i]);
+  }
+}
+
+// per-channel dy = A·dz + D·y + E, dγ, dβ from the reduced sums
+__global__ void bn_bwd_coef_kernel(const double* __restrict__ sums, int nsets, int C, double count,
+                                   const float* __restrict__ g_a, const float* __restrict__ mean_a,
+                                   const float* __restrict__ inv_a, const float* __restrict__ g_b,
+                                   const float* __restrict__ mean_b, const float* __restrict__ inv_b,
+                                   float* __restrict__ coef_a, float* __restrict__ coef_b,
+                                   float* __restrict__ dgamma_a, float* __restrict__ dbeta_a,
+                                   float* __restrict__ dgamma_b, float* __restrict__ dbeta_b) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sdz = sums[c];
+  for (int set = 0; set < nsets; ++set) {
+    const float* gg = set == 0 ? g_a : g_b;
+    const float* mm = set == 0 ? mean_a : mean_b;
+    const float* iv = set == 0 ? inv_a : inv_b;
+    float* coef = set == 0 ? coef_a : coef_b;
+    const double sdzy = sums[(size_t)(1 + set) * C + c];
+    const double inv = iv[c], mu = mm[c], gam = gg ? gg[c] : 1.0;
+    const double A = gam * inv;
+    const double m1 = sdz / count, m2 = sdzy / count;
+    const double D = -A * inv * inv * m2;
+    const double E = -A * m1 - D * mu;
+    coef[c] = (float)A;
+    coef[C + c] = (float)D;
+    coef[2 * C + c] = (float)E;
+    float* dg = set == 0 ? dgamma_a : dgamma_b;
+    float* db = set == 0 ? dbeta_a : dbeta_b;
+    if (dg) dg[c] = (float)(sdzy * inv);
+    if (db) db[c] = (float)sdz;
+  }
+}
+
+template <bool TWO>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout,
+                                                           const uint16_t* __restrict__ outv,
+                                                           const uint16_t* __restrict__ ya, const float* __restrict__ ca,
+                                                           const uint16_t* __restrict__ yb, const float* __restrict__ cb,
+                                                           uint16_t* __restrict__ dya, uint16_t* __restrict__ dyb,
+                                                           uint16_t* __restrict__ dz_out, long n8, int C8, int C) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n8; e += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(e % C8) * 8;
+    float d[8], a[8], r[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[e], d);
+    if (outv) {
+      float o[8];
+      unpack8(reinterpret_cast<const uint4*>(outv)[e], o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
+    }
+    if (dz_out) reinterpret_cast<uint4*>(dz_out)[e] = pack8(d);
+    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = ca[c0 + i] * d[i] + ca[C + c0 + i] * a[i] + ca[2 * C + c0 + i];
+    reinterpret_cast<uint4*>(dya)[e] = pack8(r);
+    if (TWO) {
+      unpack8(reinterpret_cast<const uint4*>(yb)[e], a);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = cb[c0 + i] * d[i] + cb[C + c0 + i] * a[i] + cb[2 * C + c0 + i];
+      reinterpret_cast<uint4*>(dyb)[e] = pack8(r);
+    }
+  }
+}
+
+int ew_grid(long n8) {
+  long g = (n8 + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(double) * 2 * C, s);
+  if (e != hipSuccess) return e;
+  int gy = (rows + 127) / 128;   // >= 32 rows per thread-row
+  if (gy > 64) gy = 64;
+  if (gy < 1) gy = 1;
+  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((2 * C + 63) / 64, gy), dim3(256), 0, s, slab, rows, C, out);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bn_finalize(const double* sums, int C, double count, const float* gamma, const float* beta,
+                              float eps, float momentum, int update_running, float* running_mean, float* running_var,
+                              float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, C, count, gamma, beta, eps,
+                     momentum, update_running, running_mean, running_var, scale, shift, mean, invstd);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                                 float eps, float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, rm, rv, eps,
+                     scale, shift);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, const void* r, const float* sc2,
+                           const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s) {
+  const long n8 = numel / 8;
+  const int C8 = C / 8;
+  const dim3 grid(ew_grid(n8)), blk(256);
+  const uint16_t* yy = (const uint16_t*)y;
+  const uint16_t* rr = (const uint16_t*)r;
+  uint16_t* oo = (uint16_t*)out;
+#define SDX_APPLY(RM, RL) hipLaunchKernelGGL((bn_apply_kernel<RM, RL>), grid, blk, 0, s, yy, sc, sh, rr, sc2, sh2, oo, n8, C8)
+  if (res_mode == 0) { if (relu) SDX_APPLY(0, true); else SDX_APPLY(0, false); }
+  else if (res_mode == 1) { if (relu) SDX_APPLY(1, true); else SDX_APPLY(1, false); }
+  else { if (relu) SDX_APPLY(2, true); else SDX_APPLY(2, false); }
+#undef SDX_APPLY
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
+                                const float* mb, long numel, int C, double* sums, hipStream_t s) {
+  const int nsets = yb ? 3 : 2;
+  hipError_t e = hipMemsetAsync(sums, 0, sizeof(double) * nsets * C, s);
+  if (e != hipSuccess) return e;
+  const long n8 = numel / 8;
+  const int C8 = C / 8;
+  // grid stride must be a multiple of C8 (fixed channel group per thread): 256 % C8 == 0
+  long g = (n8 + 256 * 8 - 1) / (256 * 8);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  if (yb)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
+                       (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)yb, mb, n8, C8, C, sums);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
+                       (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)nullptr, (const float*)nullptr,
+                       n8, C8, C, sums);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
+                              const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
+                              const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
+                              float* dgamma_b, float* dbeta_b, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, nsets, C, count, g_a, mean_a,
+                     inv_a, g_b, mean_b, inv_b, coef_a, coef_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
+                               const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s) {
+  const long n8 = numel / 8;
+  const int C8 = C / 8;
+  if (yb)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
+                       (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)yb, cb, (uint16_t*)dya,
+                       (uint16_t*)dyb, (uint16_t*)dz_out, n8, C8, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
+                       (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)nullptr, (const float*)nullptr,
+                       (uint16_t*)dya, (uint16_t*)nullptr, (uint16_t*)dz_out, n8, C8, C);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}

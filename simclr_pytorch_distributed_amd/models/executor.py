@@ -1,0 +1,114 @@
+"""Execution of the ResNet modules on the native gfx950 path.
+
+The modules in ``models/resnet.py`` own parameters/buffers with the reference's names;
+this executor walks them and issues the fused native ops instead of ``nn.Conv2d`` /
+``nn.BatchNorm2d``:
+
+* activations NHWC bf16, produced and consumed by the implicit-GEMM MFMA conv kernels;
+* every conv (training) emits its BN statistics from the epilogue; every BN+ReLU (and
+  BN+shortcut-BN+add+ReLU) is one fused elementwise pass; SyncBN adds one fp64
+  all-reduce per BN;
+* global average pooling and the projection head run as stock torch ops on the
+  [views, 2048] feature matrix (tiny compared to the trunk).
+
+Reference forward: networks/resnet_big.py:57-67 (Bottleneck), 24-35 (BasicBlock),
+110-118 (ResNet), 177-181 (SupConResNet).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..ops.bn import bn_act, bn_add_act
+from ..ops.conv import conv2d_nhwc
+from .resnet import BasicBlock, Bottleneck, ResNet
+
+INPUT_CHANNELS_PADDED = 8   # NHWC input images carry 3 channels padded to 8 (16-byte rows)
+
+
+def _bottleneck(b: Bottleneck, x, training, group):
+    st = training
+    y1, s1 = conv2d_nhwc(x, b.conv1.weight, 1, 0, st)
+    a1 = bn_act(y1, s1, b.bn1, True, training, group)
+    y2, s2 = conv2d_nhwc(a1, b.conv2.weight, b.stride, 1, st)
+    a2 = bn_act(y2, s2, b.bn2, True, training, group)
+    y3, s3 = conv2d_nhwc(a2, b.conv3.weight, 1, 0, st)
+    if len(b.shortcut) > 0:
+        ys, ss = conv2d_nhwc(x, b.shortcut[0].weight, b.stride, 0, st)
+        return bn_add_act(y3, s3, b.bn3, ys, ss, b.shortcut[1], None, training, group)
+    return bn_add_act(y3, s3, b.bn3, x=x, training=training, group=group)
+
+
+def _basic(b: BasicBlock, x, training, group):
+    st = training
+    y1, s1 = conv2d_nhwc(x, b.conv1.weight, b.stride, 1, st)
+    a1 = bn_act(y1, s1, b.bn1, True, training, group)
+    y2, s2 = conv2d_nhwc(a1, b.conv2.weight, 1, 1, st)
+    if len(b.shortcut) > 0:
+        ys, ss = conv2d_nhwc(x, b.shortcut[0].weight, b.stride, 0, st)
+        return bn_add_act(y2, s2, b.bn2, ys, ss, b.shortcut[1], None, training, group)
+    return bn_add_act(y2, s2, b.bn2, x=x, training=training, group=group)
+
+
+def encoder_forward_native(enc: ResNet, x_nhwc: torch.Tensor, training: bool = True, group=None) -> torch.Tensor:
+    """``x_nhwc``: [N, H, W, 8] bf16 (3 real channels). Returns fp32 [N, feat_dim]."""
+    if enc.stem != "cifar":
+        raise NotImplementedError("native path: ImageNet stem (7x7/2 + maxpool) not implemented yet")
+    cin = enc.conv1.weight.shape[1]
+    pad_c = x_nhwc.shape[-1] - cin
+    y, s = conv2d_nhwc(x_nhwc, enc.conv1.weight, 1, 1, training, cin_pad=pad_c)
+    out = bn_act(y, s, enc.bn1, True, training, group)
+    for blk in enc.blocks():
+        if isinstance(blk, Bottleneck):
+            out = _bottleneck(blk, out, training, group)
+        else:
+            out = _basic(blk, out, training, group)
+    return out.float().mean(dim=(1, 2))
+
+
+def head_forward(head, feat: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """Projection head in ``dtype`` with fp32 master weights (networks/resnet_big.py:168-172)."""
+    if isinstance(head, torch.nn.Linear):
+        return F.linear(feat.to(dtype), head.weight.to(dtype), head.bias.to(dtype)).float()
+    l1, l2 = head[0], head[2]
+    h = F.relu(F.linear(feat.to(dtype), l1.weight.to(dtype), l1.bias.to(dtype)))
+    return F.linear(h, l2.weight.to(dtype), l2.bias.to(dtype)).float()
+
+
+def to_nhwc_input(images: torch.Tensor, c_pad: int = INPUT_CHANNELS_PADDED) -> torch.Tensor:
+    """NCHW float images -> NHWC bf16 with channels zero-padded to ``c_pad``."""
+    x = images.permute(0, 2, 3, 1)
+    if x.shape[-1] < c_pad:
+        x = F.pad(x, (0, c_pad - x.shape[-1]))
+    return x.to(torch.bfloat16).contiguous()
+
+
+class ModelRunner:
+    """Runs a ``SupConResNet`` (or just its encoder) on the chosen backend.
+
+    ``backend='torch'`` calls the modules (NCHW, autocast bf16 on GPU when requested);
+    ``backend='native'`` uses the gfx950 kernels above. Inputs to :meth:`forward` are
+    NCHW float images for ``torch`` and NHWC bf16 (C padded to 8) for ``native``.
+    """
+
+    def __init__(self, model, backend: str = "native", precision: str = "bf16", sync_group=None):
+        self.model = model
+        self.backend = backend
+        self.precision = precision
+        self.sync_group = sync_group
+
+    def encode(self, x, training=None):
+        enc = self.model.encoder
+        training = enc.training if training is None else training
+        if self.backend == "native":
+            return encoder_forward_native(enc, x, training, self.sync_group)
+        if x.is_cuda and self.precision == "bf16":
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return enc(x).float()
+        return enc(x)
+
+    def forward(self, x):
+        feat = self.encode(x)
+        if self.backend == "native" or (x.is_cuda and self.precision == "bf16"):
+            return head_forward(self.model.head, feat)
+        return self.model.head(feat)

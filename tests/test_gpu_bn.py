@@ -1,0 +1,81 @@
+"""Fused BatchNorm kernels vs torch.batch_norm in fp32 (GPU)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("res_mode", [0, 1, 2])
+def test_bn_train_fwd_bwd(gpu, res_mode):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(0)
+    N, H, W, C = 16, 8, 8, 128
+    y = (torch.randn(N, H, W, C, device=gpu) * 2 + 0.5).bfloat16()
+    y2 = (torch.randn(N, H, W, C, device=gpu) - 1).bfloat16()
+    g1 = torch.rand(C, device=gpu) + 0.5
+    b1 = torch.randn(C, device=gpu)
+    g2 = torch.rand(C, device=gpu) + 0.5
+    b2 = torch.randn(C, device=gpu)
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    rm2, rv2 = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+
+    # reference in fp32 NCHW
+    yf = y.float().permute(0, 3, 1, 2).requires_grad_(True)
+    y2f = y2.float().permute(0, 3, 1, 2).requires_grad_(True)
+    g1r, b1r, g2r, b2r = [t.clone().requires_grad_(True) for t in (g1, b1, g2, b2)]
+    rmr, rvr = rm.clone(), rv.clone()
+    o = F.batch_norm(yf, rmr, rvr, g1r, b1r, training=True, momentum=0.1, eps=1e-5)
+    if res_mode == 1:
+        o = o + F.batch_norm(y2f, rm2.clone(), rv2.clone(), g2r, b2r, training=True, momentum=0.1, eps=1e-5)
+    elif res_mode == 2:
+        o = o + y2f
+    o = F.relu(o)
+    dout = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    o.backward(dout.float().permute(0, 3, 1, 2))
+
+    # native
+    count = N * H * W
+    flat = y.reshape(-1, C).float()
+    sums = torch.stack([flat.sum(0), (flat * flat).sum(0)]).double().contiguous()
+    sc, sh, mean, inv = m.bn_finalize(sums, float(count), g1, b1, 1e-5, 0.1, True, rm, rv)
+    sc2 = sh2 = mean2 = inv2 = None
+    if res_mode == 1:
+        flat2 = y2.reshape(-1, C).float()
+        sums2 = torch.stack([flat2.sum(0), (flat2 * flat2).sum(0)]).double().contiguous()
+        sc2, sh2, mean2, inv2 = m.bn_finalize(sums2, float(count), g2, b2, 1e-5, 0.1, True, rm2, rv2)
+    out = m.bn_apply(y, sc, sh, y2 if res_mode else None, sc2, sh2, res_mode, True)
+    assert _rel(out.permute(0, 3, 1, 2), o.detach()) < 1e-2
+    assert torch.allclose(rm, rmr, atol=1e-4) and torch.allclose(rv, rvr, rtol=1e-3)
+
+    do = dout.contiguous()
+    two = res_mode == 1
+    s = m.bn_bwd_reduce(do, out, y, mean, y2 if two else None, mean2 if two else None)
+    ca, cb, dga, dba, dgb, dbb = m.bn_bwd_coef(s, float(count), g1, mean, inv, g2 if two else None,
+                                               mean2 if two else None, inv2 if two else None)
+    dya, dyb, dz = m.bn_bwd_apply(do, out, y, ca, y2 if two else None, cb if two else None, res_mode == 2)
+    assert _rel(dya.permute(0, 3, 1, 2), yf.grad) < 2e-2
+    assert _rel(dga, g1r.grad) < 1e-2 and _rel(dba, b1r.grad) < 1e-2
+    if two:
+        assert _rel(dyb.permute(0, 3, 1, 2), y2f.grad) < 2e-2
+        assert _rel(dgb, g2r.grad) < 1e-2 and _rel(dbb, b2r.grad) < 1e-2
+    if res_mode == 2:
+        assert _rel(dz.permute(0, 3, 1, 2), y2f.grad) < 1e-2
+
+
+def test_bn_eval_affine(gpu):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    C = 64
+    rm, rv = torch.randn(C, device=gpu), torch.rand(C, device=gpu) + 0.1
+    g, b = torch.randn(C, device=gpu), torch.randn(C, device=gpu)
+    sc, sh = m.bn_eval_affine(g, b, rm, rv, 1e-5)
+    y = torch.randn(4, 4, 4, C, device=gpu).bfloat16()
+    out = m.bn_apply(y, sc, sh, None, None, None, 0, False)
+    ref = F.batch_norm(y.float().permute(0, 3, 1, 2), rm, rv, g, b, training=False, eps=1e-5)
+    assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2

@@ -1,0 +1,90 @@
+"""Implicit-GEMM MFMA convolution kernels vs fp32 torch convolution (GPU)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+# (N, H, W, C, K, R, stride, pad)
+SHAPES = [
+    (4, 8, 8, 64, 64, 1, 1, 0),
+    (3, 8, 8, 64, 256, 1, 1, 0),
+    (2, 9, 7, 128, 64, 3, 1, 1),     # ragged spatial, M tail
+    (4, 8, 8, 64, 128, 3, 2, 1),     # strided 3x3
+    (4, 8, 8, 256, 512, 1, 2, 0),    # strided 1x1 shortcut
+    (8, 8, 8, 8, 64, 3, 1, 1),       # stem (C padded to 8)
+    (2, 4, 4, 512, 512, 3, 1, 1),    # layer4 shape
+]
+
+
+def _mk(N, H, W, C, K, R, seed=0, dev="cuda"):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(N, C, H, W, generator=g).to(dev).bfloat16()
+    w = (torch.randn(K, C, R, R, generator=g) / (C * R * R) ** 0.5).to(dev).bfloat16()
+    return x, w
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_conv_fwd(gpu, shape, cfg):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, W, C, K, R, st, pad = shape
+    x, w = _mk(N, H, W, C, K, R)
+    ref = F.conv2d(x.float(), w.float(), stride=st, padding=pad)                  # NCHW fp32
+    xh = x.permute(0, 2, 3, 1).contiguous()
+    wh = w.permute(0, 2, 3, 1).contiguous()
+    y, slab = m.conv_fwd(xh, wh, st, pad, True, cfg)
+    yr = y.permute(0, 3, 1, 2).float()
+    assert _rel(yr, ref) < 1e-2
+    sums = m.bn_stats_reduce(slab)
+    yf = y.float().reshape(-1, K)
+    assert torch.allclose(sums[0].float(), yf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sums[1].float(), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_conv_dgrad(gpu, shape, cfg):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, W, C, K, R, st, pad = shape
+    x, w = _mk(N, H, W, C, K, R)
+    xf = x.float().requires_grad_(True)
+    out = F.conv2d(xf, w.float(), stride=st, padding=pad)
+    dy = torch.randn_like(out).bfloat16()
+    (dx_ref,) = torch.autograd.grad(out, xf, dy.float())
+    wt = w.permute(1, 2, 3, 0).contiguous()            # [C][R][S][K]
+    dx = m.conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), wt, H, W, st, pad, cfg)
+    assert _rel(dx.permute(0, 3, 1, 2), dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_conv_wgrad(gpu, shape, cfg):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, W, C, K, R, st, pad = shape
+    x, w = _mk(N, H, W, C, K, R)
+    wf = w.float().requires_grad_(True)
+    out = F.conv2d(x.float(), wf, stride=st, padding=pad)
+    dy = torch.randn_like(out).bfloat16()
+    (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
+    for splits in (1, 3):
+        dw = m.conv_wgrad(dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous(), R, R, st, pad,
+                          splits, cfg)
+        assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
+
+
+def test_conv_large_m(gpu):
+    """Layer-1 scale (M = 512·32·32) against torch bf16 conv."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    x, w = _mk(64, 32, 32, 64, 64, 3)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    y, _ = m.conv_fwd(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).contiguous(), 1, 1, False, -1)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
