@@ -221,9 +221,11 @@ torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, tor
     mbp = mb->data_ptr<float>();
   }
   c10::DeviceGuard dg(dout.device());
-  auto sums = torch::empty({ybp ? 3 : 2, C}, dout.options().dtype(at::kDouble));
+  const int nsets = ybp ? 3 : 2;
+  auto sums = torch::empty({nsets, C}, dout.options().dtype(at::kDouble));
+  auto partial = torch::empty({bn_bwd_reduce_blocks(dout.numel(), C), nsets, C}, dout.options().dtype(at::kFloat));
   check_hip(launch_bn_bwd_reduce(dout.data_ptr(), op, ya.data_ptr(), ma.data_ptr<float>(), ybp, mbp, dout.numel(), C,
-                                 sums.data_ptr<double>(), cur_stream()),
+                                 partial.data_ptr<float>(), sums.data_ptr<double>(), cur_stream()),
             "bn_bwd_reduce");
   return sums;
 }

@@ -1,0 +1,52 @@
+// Bindings for the fused flat-buffer optimizers (optim.hip).
+#include "ops_decl.h"
+#include "launchers.h"
+
+namespace sdx_bind {
+namespace {
+
+void check_flat(const torch::Tensor& t, int64_t n, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 1 && t.numel() == n,
+              name, " must be a contiguous flat float32 GPU tensor of the parameter size");
+}
+
+void sgd_step(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor lr, double momentum, double wd,
+              double gscale, bool nesterov) {
+  const int64_t n = p.numel();
+  check_flat(p, n, "p");
+  check_flat(g, n, "g");
+  check_flat(buf, n, "buf");
+  TORCH_CHECK(n % 4 == 0, "flat size must be a multiple of 4");
+  TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == at::kFloat && lr.numel() == 1, "lr must be a GPU float scalar");
+  c10::DeviceGuard dg(p.device());
+  check_hip(launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), n, lr.data_ptr<float>(),
+                       (float)momentum, (float)wd, (float)gscale, nesterov ? 1 : 0, cur_stream()),
+            "sgd_step");
+}
+
+void lars_step(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor seg_off, torch::Tensor adapt,
+               torch::Tensor lr, double momentum, double wd, double gscale, double eta, torch::Tensor norms) {
+  const int64_t n = p.numel();
+  check_flat(p, n, "p");
+  check_flat(g, n, "g");
+  check_flat(buf, n, "buf");
+  const int64_t nseg = seg_off.numel();
+  TORCH_CHECK(seg_off.is_cuda() && seg_off.scalar_type() == at::kLong && seg_off.is_contiguous(), "seg_off int64");
+  TORCH_CHECK(adapt.is_cuda() && adapt.scalar_type() == at::kInt && adapt.numel() == nseg, "adapt int32[nseg]");
+  TORCH_CHECK(norms.is_cuda() && norms.scalar_type() == at::kFloat && norms.numel() == 2 * nseg, "norms [2*nseg]");
+  TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == at::kFloat && lr.numel() == 1, "lr must be a GPU float scalar");
+  c10::DeviceGuard dg(p.device());
+  check_hip(launch_lars(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), seg_off.data_ptr<int64_t>(),
+                        adapt.data_ptr<int>(), (int)nseg, n, lr.data_ptr<float>(), (float)momentum, (float)wd,
+                        (float)gscale, (float)eta, norms.data_ptr<float>(), cur_stream()),
+            "lars_step");
+}
+
+}  // namespace
+
+void register_optim(pybind11::module& m) {
+  m.def("sgd_step", &sgd_step, "fused flat-buffer SGD (momentum, wd, grad scale, device lr)");
+  m.def("lars_step", &lars_step, "fused flat-buffer LARS");
+}
+
+}  // namespace sdx_bind

@@ -46,8 +46,9 @@ hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, c
                                  float eps, float* scale, float* shift, hipStream_t s);
 hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, const void* r, const float* sc2,
                            const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s);
+int bn_bwd_reduce_blocks(long numel, int C);
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
-                                const float* mb, long numel, int C, double* sums, hipStream_t s);
+                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s);
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
                               const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
                               const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
@@ -61,3 +62,10 @@ hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, in
                               float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
                               float sat, float hue, float gray_p, int do_crop, int do_flip, void* out,
                               hipStream_t s);
+
+// ---- optimizers (optim.hip) -----------------------------------------------------
+hipError_t launch_sgd(float* p, const float* g, float* buf, long n, const float* lr, float momentum, float wd,
+                      float gscale, int nesterov, hipStream_t s);
+hipError_t launch_lars(float* p, const float* g, float* buf, const long* seg_off, const int* adapt, int nseg, long n,
+                       const float* lr, float momentum, float wd, float gscale, float eta, float* norms,
+                       hipStream_t s);

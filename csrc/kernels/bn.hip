@@ -33,21 +33,22 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
 }
 
-// slab [rows][2][C] fp32 -> out [2][C] fp64 (out zeroed by the launcher)
-__global__ __launch_bounds__(256) void bn_stats_reduce_kernel(const float* __restrict__ slab, int rows, int C,
-                                                              double* __restrict__ out) {
+// slab [rows][nsets][C] fp32 -> out [nsets][C] fp64 (out zeroed by the launcher); a 2-D
+// grid bounds the atomics per address to gridDim.y.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows, int nsets, int C,
+                                                          double* __restrict__ out) {
   __shared__ double red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);   // index into [2][C]
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);   // index into [nsets][C]
   const int ty = threadIdx.x >> 6;
   double acc = 0.0;
-  if (col < 2 * C) {
+  if (col < nsets * C) {
     const int which = col / C, ch = col % C;
     for (int r = blockIdx.y * 4 + ty; r < rows; r += gridDim.y * 4)
-      acc += (double)slab[((size_t)r * 2 + which) * C + ch];
+      acc += (double)slab[((size_t)r * nsets + which) * C + ch];
   }
   red[ty][threadIdx.x & 63] = acc;
   __syncthreads();
-  if (ty == 0 && col < 2 * C) {
+  if (ty == 0 && col < nsets * C) {
     const double s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     atomicAdd(out + col, s);
   }
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ outv,
                                                             const uint16_t* __restrict__ ya, const float* __restrict__ ma,
                                                             const uint16_t* __restrict__ yb, const float* __restrict__ mb,
-                                                            long n8, int C8, int C, double* __restrict__ sums) {
+                                                            long n8, int C8, int C, float* __restrict__ partial) {
   constexpr int NS = TWO ? 3 : 2;
   __shared__ float red[NS][256][8];
   const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -193,11 +194,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       for (int q = 0; q < NS; ++q)
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[q][i] += red[q][t][i];
-    const int g0 = (int)((blockIdx.x * (long)blockDim.x + threadIdx.x) % C8) * 8;
+    const int g0 = (int)threadIdx.x * 8;
 #pragma unroll
     for (int q = 0; q < NS; ++q)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) atomicAdd(sums + (size_t)q * C + g0 + i, acc[q][i]);
+      for (int i = 0; i < 8; ++i) partial[((size_t)blockIdx.x * NS + q) * C + g0 + i] = (float)acc[q][i];
   }
 }
 
@@ -273,15 +274,19 @@ int ew_grid(long n8) {
 
 }  // namespace
 
-hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(out, 0, sizeof(double) * 2 * C, s);
+static hipError_t launch_slab_reduce(const float* slab, int rows, int nsets, int C, double* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(double) * nsets * C, s);
   if (e != hipSuccess) return e;
   int gy = (rows + 127) / 128;   // >= 32 rows per thread-row
   if (gy > 64) gy = 64;
   if (gy < 1) gy = 1;
-  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((2 * C + 63) / 64, gy), dim3(256), 0, s, slab, rows, C, out);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((nsets * C + 63) / 64, gy), dim3(256), 0, s, slab, rows, nsets, C, out);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
+}
+
+hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s) {
+  return launch_slab_reduce(slab, rows, 2, C, out, s);
 }
 
 hipError_t launch_bn_finalize(const double* sums, int C, double count, const float* gamma, const float* beta,
@@ -318,26 +323,31 @@ hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, cons
   return hipSuccess;
 }
 
+int bn_bwd_reduce_blocks(long numel, int C) {
+  const long n8 = numel / 8;
+  long g = (n8 + 256 * 16 - 1) / (256 * 16);   // ~16 chunks per thread
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  (void)C;
+  return (int)g;
+}
+
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
-                                const float* mb, long numel, int C, double* sums, hipStream_t s) {
+                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s) {
   const int nsets = yb ? 3 : 2;
-  hipError_t e = hipMemsetAsync(sums, 0, sizeof(double) * nsets * C, s);
-  if (e != hipSuccess) return e;
   const long n8 = numel / 8;
   const int C8 = C / 8;
   // grid stride must be a multiple of C8 (fixed channel group per thread): 256 % C8 == 0
-  long g = (n8 + 256 * 8 - 1) / (256 * 8);
-  if (g > 2048) g = 2048;
-  if (g < 1) g = 1;
+  const int g = bn_bwd_reduce_blocks(numel, C);
   if (yb)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
-                       (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)yb, mb, n8, C8, C, sums);
+                       (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)yb, mb, n8, C8, C, partial);
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)nullptr, (const float*)nullptr,
-                       n8, C8, C, sums);
+                       n8, C8, C, partial);
   SDX_LAUNCH_CHECK();
-  return hipSuccess;
+  return launch_slab_reduce(partial, g, nsets, C, sums, s);
 }
 
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,

@@ -1,0 +1,268 @@
+"""Contrastive pretraining engine (SimCLR / SupCon) — replaces main_supcon.py:155-406.
+
+Per step (reference hot loop: main_supcon.py:253-349):
+
+1. the rank's slice of the epoch permutation indexes the HBM-resident uint8 dataset and
+   the fused GPU augmentation kernel writes both views (NHWC bf16) — no DataLoader
+   workers, no H2D copy (reference: 8 CPU workers running PIL, main_supcon.py:200-207);
+2. per-iteration warm-up lr (util.py:69-76) is written to the optimizer's device lr;
+3. forward: native gfx950 encoder (or stock torch ops) + projection head;
+4. loss: row-owned distributed SupCon/NT-Xent over globally gathered embeddings
+   (losses/supcon.py) + the optional SEC / L2-reg feature-norm terms (main_supcon.py:295-317);
+5. backward with bucketed gradient all-reduce overlapped on a comm stream
+   (parallel/ddp.py), then one fused SGD/LARS kernel over the flat parameter buffer.
+
+Logging keeps the reference's console format and TensorBoard tags; metric values stay on
+device and are synchronised only every ``print_freq`` steps.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import sys
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..data.augment import AugConfig, augment, nhwc8_to_nchw
+from ..data.datasets import build_dataset
+from ..data.sampler import DistributedIndexSampler
+from ..losses.supcon import DistributedContrastiveLoss
+from ..models.executor import ModelRunner
+from ..models.resnet import SupConResNet
+from ..ops import _ext
+from ..optim.flat import FlatParams, build_optimizer
+from ..optim.schedules import adjust_learning_rate, warmup_learning_rate
+from ..parallel import comm
+from ..parallel.ddp import GradBucketReducer
+from ..utils.logging import setup_logging
+from ..utils.meters import AverageMeter
+from . import checkpoint as ckpt_mod
+
+
+def resolve_backend(requested: str, device: torch.device, stem: str = "cifar") -> str:
+    if requested == "torch":
+        return "torch"
+    native_ok = device.type == "cuda" and _ext.available() and stem == "cifar"
+    if requested == "native":
+        if not native_ok:
+            _ext.require()
+            raise RuntimeError("native backend needs a GPU and the CIFAR stem")
+        return "native"
+    return "native" if native_ok else "torch"
+
+
+def step_seed(base: int, epoch: int, idx: int, rank: int) -> int:
+    return (base * 1000003 + epoch * 100003 + idx * 17 + rank * 7919) & ((1 << 62) - 1)
+
+
+class PretrainEngine:
+    def __init__(self, opt, device: Optional[torch.device] = None):
+        self.opt = opt
+        rank, local_rank, world, dev = comm.init_distributed(opt.dist_backend, device=device)
+        self.rank, self.world, self.device = rank, world, dev
+        if opt.ngpu != world and world > 1:
+            logging.warning(f"--ngpu {opt.ngpu} != launcher WORLD_SIZE {world}; using {world}")
+        opt.world_size = world
+        opt.local_batch = opt.batch_size // world
+        setup_logging(opt.save_folder, rank)
+        if rank == 0:
+            logging.info(f"create {opt.conf_work_path} ...")
+        torch.manual_seed(opt.seed)
+        self.backend = resolve_backend(opt.backend, dev, opt.stem)
+
+        model = SupConResNet(opt.model, opt.head, opt.feat_dim, opt.stem)
+        if opt.ckpt:
+            sd = ckpt_mod.load_checkpoint(opt.ckpt)["model"]
+            ckpt_mod.load_model_state(model, sd)
+            logging.info(f"load model from {opt.ckpt} ...")
+        self.sync_group = None
+        if opt.syncBN and world > 1:
+            if self.backend == "torch":
+                from ..parallel.syncbn import convert_sync_bn
+                model = convert_sync_bn(model)
+            else:
+                self.sync_group = dist.group.WORLD
+        model = model.to(dev)
+        if dev.type == "cuda":
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
+        self.flat = FlatParams(model)
+        self.optimizer = build_optimizer(opt.optimizer, self.flat, opt.learning_rate, opt.momentum,
+                                         opt.weight_decay, backend="torch" if self.backend == "torch" else "auto")
+        self.reducer = GradBucketReducer(self.flat) if world > 1 else None
+        self.optimizer.grad_scale = (1.0 / world) if opt.grad_semantics == "ref" else 1.0
+        self.runner = ModelRunner(model, self.backend, opt.precision, self.sync_group)
+        self.criterion = DistributedContrastiveLoss(opt.method, opt.temp, opt.base_temperature, opt.contrast_mode,
+                                                    backend="native" if self.backend == "native" else "torch")
+        # data: whole uint8 dataset resident on the device
+        ds = build_dataset(opt.dataset, opt.data_folder, True, opt.synthetic, opt.synthetic_size, opt.size, opt.seed)
+        self.data = torch.from_numpy(ds.images).to(dev)
+        self.labels = torch.from_numpy(ds.labels).to(dev)
+        self.sampler = DistributedIndexSampler(len(ds), opt.local_batch, world, rank, seed=opt.seed)
+        self.aug = AugConfig.simclr(opt.size, opt.mean_t, opt.std_t)
+        self.logger = None
+        if rank == 0:
+            from ..utils.tb import Logger
+            self.logger = Logger(opt.tb_folder, flush_secs=2)
+        self.start_epoch = 1
+        self.global_step = 0
+        self.record_norm_mean: Optional[torch.Tensor] = None
+        if getattr(opt, "resume", ""):
+            self._resume(opt.resume)
+
+    # ------------------------------------------------------------------------------
+    def _resume(self, path):
+        st = ckpt_mod.load_checkpoint(path)
+        ckpt_mod.load_model_state(self.model, st["model"])
+        self.optimizer.load_state_dict(st["optimizer"])
+        self.start_epoch = int(st["epoch"]) + 1
+        extra = st.get("sdx_state") or {}
+        self.global_step = int(extra.get("global_step", 0))
+        rnm = extra.get("record_norm_mean")
+        if rnm is not None:
+            self.record_norm_mean = torch.tensor(float(rnm), device=self.device)
+        logging.info(f"resumed from {path} at epoch {self.start_epoch}")
+
+    def _extra_state(self, epoch):
+        return {"global_step": self.global_step, "epoch": epoch,
+                "record_norm_mean": None if self.record_norm_mean is None else float(self.record_norm_mean)}
+
+    # ------------------------------------------------------------------------------
+    def make_views(self, idx: torch.Tensor, epoch: int, it: int) -> torch.Tensor:
+        x = augment(self.data, idx, self.aug, step_seed(self.opt.seed, epoch, it, self.rank))
+        if self.backend == "torch":
+            x = nhwc8_to_nchw(x)
+        return x
+
+    def train_step(self, idx: torch.Tensor, epoch: int, it: int, iters: int):
+        opt = self.opt
+        x = self.make_views(idx, epoch, it)
+        labels = self.labels[idx]
+        warmup_learning_rate(opt, epoch, it, iters, self.optimizer)
+        feats = self.runner.forward(x)
+        loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
+        stats = self._norm_terms(feats, epoch, it, iters)
+        loss = loss + stats.pop("extra_loss")
+        self.optimizer.zero_grad()
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        self.optimizer.step()
+        self.global_step += 1
+        stats["loss_local"] = loss.detach()
+        return stats
+
+    def _norm_terms(self, feats, epoch, it, iters):
+        """SEC / L2-reg regularisers on un-normalised global features (main_supcon.py:295-317)."""
+        opt = self.opt
+        norms = feats.float().norm(dim=1)
+        n_global = norms.numel() * self.world
+        local = torch.stack([norms.sum(), (norms * norms).sum()])
+        need_global = opt.sec or opt.l2reg
+        if need_global and self.world > 1:
+            g = local.detach().clone()
+            comm.all_reduce_sum_(g)
+        else:
+            g = local.detach() * (self.world if self.world > 1 else 1)
+        norm_mean = g[0] / n_global
+        norm_var = g[1] / n_global - norm_mean * norm_mean
+        if self.record_norm_mean is None:
+            self.record_norm_mean = norm_mean.detach()
+        else:
+            m = opt.norm_momentum
+            self.record_norm_mean = (1 - m) * self.record_norm_mean + m * norm_mean.detach()
+        now_iter = (epoch - 1) * iters + it
+        ramp = now_iter / (opt.epochs * iters)
+        extra = torch.zeros((), device=feats.device)
+        loss_sec = ((norms - self.record_norm_mean) ** 2).sum() / n_global
+        loss_l2 = (norms ** 2).sum() / n_global
+        if opt.sec:
+            extra = extra + opt.sec_wei * ramp * loss_sec
+        if opt.l2reg:
+            extra = extra + opt.l2reg_wei * ramp * loss_l2
+        return {"extra_loss": extra, "norm_mean": norm_mean.detach(), "norm_var": norm_var.detach(),
+                "loss_sec": loss_sec.detach(), "loss_l2reg": loss_l2.detach(),
+                "record_norm_mean": self.record_norm_mean.detach()}
+
+    # ------------------------------------------------------------------------------
+    def train_epoch(self, epoch: int) -> float:
+        opt = self.opt
+        self.model.train()
+        self.sampler.set_epoch(epoch)
+        iters = len(self.sampler)
+        if opt.max_steps:
+            iters = min(iters, opt.max_steps)
+        batch_time, data_time, losses = AverageMeter(), AverageMeter(), AverageMeter()
+        loss_acc = torch.zeros((), device=self.device)
+        window_loss = torch.zeros((), device=self.device)
+        window_n = 0
+        end = time.time()
+        t_window = time.time()
+        for it, idx in enumerate(self.sampler.batches(self.device)):
+            if it >= iters:
+                break
+            data_time.update(time.time() - end)
+            st = self.train_step(idx, epoch, it, iters)
+            loss_acc += st["loss_local"]
+            window_loss += st["loss_local"]
+            window_n += 1
+            batch_time.update(time.time() - end)
+            end = time.time()
+            if (it + 1) % opt.print_freq == 0 or it + 1 == iters:
+                vals = torch.stack([window_loss, st["norm_mean"], st["record_norm_mean"], st["norm_var"],
+                                    st["loss_sec"], st["loss_l2reg"], st["loss_local"]])
+                vals[0] = vals[0] / max(window_n, 1)
+                if self.world > 1:
+                    red = vals[[0, 6]].clone()
+                    comm.all_reduce_sum_(red)
+                    vals[0], vals[6] = red[0], red[1]
+                v = vals.tolist()    # one host sync per print window
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize()
+                dt = (time.time() - t_window) / window_n
+                t_window = time.time()
+                losses.update(v[0], window_n)
+                losses.val = v[6]
+                batch_time.val = dt
+                if self.rank == 0:
+                    now_iter = (epoch - 1) * iters + it
+                    for tag, k in (("info/norm_mean", 1), ("info/norm_var", 3), ("info/record_norm_mean", 2),
+                                   ("info/loss_sec", 4), ("info/loss_l2reg", 5)):
+                        self.logger.log_value(tag, v[k], now_iter)
+                    logging.info(
+                        "Train: [{0}][{1}/{2}]\tBT {bt:.3f} ({bta:.3f})\tDT {dtv:.3f} ({dta:.3f})\t"
+                        "loss {lv:.3f} ({la:.3f})\tnorm_mean {nm:.3f} (record: {rec:.3f}) var {var:.3f}\t"
+                        "img/s {ips:.0f}".format(
+                            epoch, it + 1, iters, bt=dt, bta=batch_time.avg, dtv=data_time.val, dta=data_time.avg,
+                            lv=v[6], la=losses.avg, nm=v[1], rec=v[2], var=v[3],
+                            ips=opt.batch_size / max(dt, 1e-9)))
+                    sys.stdout.flush()
+                window_loss = torch.zeros((), device=self.device)
+                window_n = 0
+        return losses.avg
+
+    def run(self):
+        opt = self.opt
+        for epoch in range(self.start_epoch, opt.epochs + 1):
+            adjust_learning_rate(opt, self.optimizer, epoch)
+            t1 = time.time()
+            loss = self.train_epoch(epoch)
+            t2 = time.time()
+            logging.info("epoch {}, total time {:.2f}".format(epoch, t2 - t1))
+            if self.rank == 0:
+                self.logger.log_value("loss", loss, epoch)
+                self.logger.log_value("learning_rate", self.optimizer.param_groups[0]["lr"], epoch)
+            if epoch % opt.save_freq == 0 and self.rank == 0:
+                f = os.path.join(opt.save_folder, f"ckpt_epoch_{epoch}.pth")
+                ckpt_mod.save_model(self.model, self.optimizer, opt, epoch, f, self._extra_state(epoch))
+            comm.barrier()
+        if self.rank == 0:
+            f = os.path.join(opt.save_folder, "last.pth")
+            ckpt_mod.save_model(self.model, self.optimizer, opt, opt.epochs, f, self._extra_state(opt.epochs))
+            self.logger.close()
+        comm.barrier()
+        return os.path.join(opt.save_folder, "last.pth")

@@ -190,7 +190,7 @@ class DistributedContrastiveLoss(nn.Module):
         w, r = comm.world_size(), comm.rank()
         nv = self.n_views
         b_local = feats.shape[0] // nv
-        n = F.normalize(feats.float(), dim=1)
+        n = F.normalize(feats.to(torch.promote_types(feats.dtype, torch.float32)), dim=1)
         C = comm.all_gather_with_grad(n)
         labels_all = None
         if self.method == "SupCon":

@@ -1,0 +1,108 @@
+"""Bucketed data-parallel gradient all-reduce, overlapped with backward.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel`` (main_supcon.py:230-234) with a
+reducer built on the flat gradient buffer of :class:`optim.flat.FlatParams`:
+
+* buckets are contiguous slices of the flat gradient (segments are laid out in backward
+  order), so each bucket is all-reduced *in place* — no copy into bucket buffers;
+* a post-accumulate-grad hook counts ready parameters; when a bucket is complete the
+  compute stream records an event, the dedicated communication stream waits on it and
+  issues the RCCL all-reduce (SUM) there, so the collective runs over xGMI while
+  backward keeps computing earlier layers;
+* averaging is not a separate pass: the optimizer kernel applies ``1/W`` (grad_scale)
+  while it streams the gradients (``--grad_semantics exact`` keeps the sum);
+* bucket size defaults to 64 MiB: on a fully connected 8-GPU xGMI node each ring step is
+  bound by one 153 GB/s link, so fewer, larger buckets amortise per-collective latency
+  (the reference's 25 MB DDP default was sized for PCIe/NVLink rings);
+* parameters/buffers are broadcast from rank 0 once at construction (one collective on
+  the flat buffer); the per-forward BN buffer broadcast of DDP is dropped.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import comm
+
+
+class GradBucketReducer:
+    def __init__(self, flat, bucket_mb: float = 64.0, group=None, enabled: Optional[bool] = None,
+                 broadcast_init: bool = True):
+        self.flat = flat
+        self.group = group
+        self.world = comm.world_size() if group is None else dist.get_world_size(group)
+        self.enabled = (self.world > 1) if enabled is None else enabled
+        cap = int(bucket_mb * (1 << 20) / 4)
+        # buckets in backward (= flat buffer) order
+        self.buckets: List[dict] = []
+        cur = None
+        for i in flat.order:
+            start = flat.offsets[i]
+            end = start + (flat.params[i].numel() + 4095) // 4096 * 4096
+            if cur is None or (end - cur["start"]) > cap and cur["params"]:
+                cur = {"start": start, "end": end, "params": [], "ready": 0, "work": None}
+                self.buckets.append(cur)
+            cur["params"].append(i)
+            cur["end"] = end
+        self.bucket_of = {}
+        for b_idx, b in enumerate(self.buckets):
+            for i in b["params"]:
+                self.bucket_of[i] = b_idx
+        self.is_cuda = flat.grad.is_cuda
+        self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (self.is_cuda and self.enabled) else None
+        self._hooks = []
+        if self.enabled:
+            for i, p in enumerate(flat.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            if broadcast_init:
+                self.broadcast_parameters()
+
+    # ---- init ---------------------------------------------------------------------
+    @torch.no_grad()
+    def broadcast_parameters(self, buffers_of: Optional[torch.nn.Module] = None):
+        if not self.enabled:
+            return
+        dist.broadcast(self.flat.flat, src=0, group=self.group)
+        mod = buffers_of if buffers_of is not None else self.flat.model
+        for b in mod.buffers():
+            dist.broadcast(b, src=0, group=self.group)
+
+    # ---- backward -----------------------------------------------------------------
+    def _make_hook(self, i):
+        def hook(_p):
+            b = self.buckets[self.bucket_of[i]]
+            b["ready"] += 1
+            if b["ready"] == len(b["params"]):
+                self._launch(b)
+        return hook
+
+    def _launch(self, b):
+        view = self.flat.grad[b["start"]:b["end"]]
+        if self.comm_stream is not None:
+            ev = torch.cuda.current_stream().record_event()
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+        else:
+            b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+
+    def finish(self):
+        """Wait for all bucket reductions (launching any bucket whose params got no grad)."""
+        if not self.enabled:
+            return
+        for b in self.buckets:
+            if b["work"] is None:
+                self._launch(b)
+        for b in self.buckets:
+            b["work"].wait()
+            b["work"] = None
+            b["ready"] = 0
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
