@@ -6,11 +6,13 @@ void register_supcon(pybind11::module& m);
 void register_conv_bn(pybind11::module& m);
 void register_data(pybind11::module& m);
 void register_optim(pybind11::module& m);
+void register_pool(pybind11::module& m);
 
 void register_ops(pybind11::module& m) {
   register_supcon(m);
   register_conv_bn(m);
   register_data(m);
   register_optim(m);
+  register_pool(m);
 }
 }  // namespace sdx_bind

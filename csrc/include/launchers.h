@@ -69,3 +69,11 @@ hipError_t launch_sgd(float* p, const float* g, float* buf, long n, const float*
 hipError_t launch_lars(float* p, const float* g, float* buf, const long* seg_off, const int* adapt, int nseg, long n,
                        const float* lr, float momentum, float wd, float gscale, float eta, float* norms,
                        hipStream_t s);
+
+// ---- pooling (pool.hip) ---------------------------------------------------------
+hipError_t launch_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C, int P, int Q, int k, int stride,
+                              int pad, hipStream_t s);
+hipError_t launch_maxpool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H, int W, int C,
+                              int P, int Q, int k, int stride, int pad, hipStream_t s);
+hipError_t launch_gap_fwd(const void* x, float* y, int N, int HW, int C, hipStream_t s);
+hipError_t launch_gap_bwd(const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
