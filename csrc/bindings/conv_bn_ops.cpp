@@ -16,10 +16,19 @@ void check_bf16_nhwc(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.numel() < (1LL << 31), name, " too large for 32-bit GEMM indexing");
 }
 
+// Pick the tile config minimising padded work, with a mild preference for the larger
+// (more MFMA-efficient) tiles: 0 128x128, 1 256x64, 2 64x256, 3 64x64.
 int auto_cfg(int64_t M, int64_t Ncol) {
-  if (Ncol <= 64) return 1;          // 256 x 64
-  if (M <= 64) return 2;             // 64 x 256
-  return 0;                          // 128 x 128
+  const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
+  const double pen[4] = {1.0, 1.04, 1.04, 1.35};
+  int best = 0;
+  double best_s = 1e300;
+  for (int c = 0; c < 4; ++c) {
+    const double padded = (double)((M + bm[c] - 1) / bm[c] * bm[c]) * (double)((Ncol + bn[c] - 1) / bn[c] * bn[c]);
+    const double s = padded * pen[c];
+    if (s < best_s) { best_s = s; best = c; }
+  }
+  return best;
 }
 
 std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
@@ -54,7 +63,7 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
 }
 
 torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                         int64_t cfg) {
+                         int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
   TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
@@ -66,15 +75,47 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
               "dgrad geometry mismatch");
   TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
   c10::DeviceGuard dg(dy.device());
-  const int64_t M = (int64_t)g.N * g.H * g.W;
+  const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
   if (cfg < 0) cfg = auto_cfg(M, g.C);
-  auto dx = torch::empty({g.N, g.H, g.W, g.C}, dy.options());
-  check_hip(launch_conv_dgrad(g, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)cfg, cur_stream()), "conv_dgrad");
+  torch::Tensor dx;
+  if (out.has_value()) {
+    dx = *out;
+    check_bf16_nhwc(dx, "out");
+    TORCH_CHECK(dx.size(0) == g.N && dx.size(1) == g.H && dx.size(2) == g.W && dx.size(3) == g.C, "out shape");
+  } else {
+    dx = torch::empty({g.N, g.H, g.W, g.C}, dy.options());
+  }
+  const void* add = nullptr;
+  if (addend.has_value()) {
+    check_bf16_nhwc(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
+    add = addend->data_ptr();
+  }
+  if (stride == 1) {
+    check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
+                                      cur_stream()),
+              "conv_dgrad");
+    return dx;
+  }
+  // sub-pixel classes: each gets the taps r ≡ ph+pad, s ≡ pw+pad (mod stride)
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      int r0, nr, s0, ns, Hc, Wc;
+      conv_dgrad_class(g, ph, pw, &r0, &nr, &s0, &ns, &Hc, &Wc);
+      torch::Tensor wc;
+      if (nr > 0 && ns > 0)
+        wc = wt.slice(1, r0, g.R, stride).slice(2, s0, g.S, stride).contiguous();
+      else
+        wc = wt;   // no taps: the kernel writes zeros and never reads B
+      check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
+                                        cur_stream()),
+                "conv_dgrad(class)");
+    }
   return dx;
 }
 
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
-                         int64_t splits, int64_t cfg) {
+                         int64_t splits, int64_t cfg, c10::optional<torch::Tensor> out, bool accumulate) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(x, "x");
   TORCH_CHECK(dy.size(0) == x.size(0), "batch mismatch");
@@ -86,17 +127,34 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
               "wgrad geometry mismatch");
   c10::DeviceGuard dg(x.device());
   const int64_t M = g.K, Ncol = (int64_t)R * S * g.C, Kd = (int64_t)g.N * g.P * g.Q;
-  if (cfg < 0) cfg = (M <= 64) ? 2 : (Ncol <= 64 ? 1 : 0);
+  if (cfg < 0) cfg = auto_cfg(M, Ncol);
   if (splits <= 0) {
     const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
                           ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
     splits = std::max<int64_t>(1, 512 / tiles);
     const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
     splits = std::min(splits, max_splits);
+    // bound the fp32 partial slab to ~64 MiB
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, (16LL << 20) / (M * Ncol)));
   }
-  auto dw = torch::zeros({g.K, R, S, g.C}, x.options().dtype(at::kFloat));
-  check_hip(launch_conv_wgrad(g, dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), (int)cfg, (int)splits,
-                              cur_stream()),
+  splits = conv_wgrad_splits(g, (int)cfg, (int)splits);
+  torch::Tensor dw;
+  if (out.has_value()) {
+    dw = *out;
+    TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.numel() == M * Ncol, "out: fp32 [K,R,S,C]");
+    const bool krsc = dw.dim() == 4 && ((dw.size(0) == g.K && dw.size(1) == g.C && dw.size(2) == R &&
+                                         dw.is_contiguous(at::MemoryFormat::ChannelsLast)) ||
+                                        (dw.size(1) == R && dw.size(3) == g.C && dw.is_contiguous()));
+    TORCH_CHECK(krsc, "out must be KRSC-contiguous (channels_last [K,C,R,S] or contiguous [K,R,S,C])");
+  } else {
+    dw = torch::empty({g.K, R, S, g.C}, x.options().dtype(at::kFloat));
+    accumulate = false;
+  }
+  torch::Tensor part;
+  if (splits > 1 || accumulate)
+    part = torch::empty({splits * M * Ncol}, x.options().dtype(at::kFloat));
+  check_hip(launch_conv_wgrad(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
+                              dw.data_ptr<float>(), (int)cfg, (int)splits, accumulate ? 1 : 0, cur_stream()),
             "conv_wgrad");
   return dw;
 }
@@ -230,8 +288,11 @@ torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, tor
   return sums;
 }
 
+// dγ/dβ go to freshly allocated tensors, or are ADDED into caller-provided gradient
+// sinks (sink_ga, sink_ba, sink_gb, sink_bb: the parameters' .grad views).
 std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_a, torch::Tensor mean_a,
-                                       torch::Tensor inv_a, OptT g_b, OptT mean_b, OptT inv_b) {
+                                       torch::Tensor inv_a, OptT g_b, OptT mean_b, OptT inv_b, OptT sink_ga,
+                                       OptT sink_ba, OptT sink_gb, OptT sink_bb) {
   TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.dim() == 2 && sums.is_contiguous(),
               "sums must be [nsets+1, C] float64");
   const int64_t C = sums.size(1);
@@ -241,14 +302,25 @@ std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_
   check_vec(inv_a, C, "inv_a");
   c10::DeviceGuard dg(sums.device());
   auto fo = sums.options().dtype(at::kFloat);
+  const bool sinks = sink_ga.has_value();
+  TORCH_CHECK(!sinks || (sink_ba.has_value() && (nsets == 1 || (sink_gb.has_value() && sink_bb.has_value()))),
+              "all gradient sinks must be given together");
   auto coef_a = torch::empty({3, C}, fo);
-  auto dga = torch::empty({C}, fo), dba = torch::empty({C}, fo);
+  torch::Tensor dga = sinks ? *sink_ga : torch::empty({C}, fo), dba = sinks ? *sink_ba : torch::empty({C}, fo);
+  if (sinks) {
+    check_vec(dga, C, "sink_ga");
+    check_vec(dba, C, "sink_ba");
+  }
   torch::Tensor coef_b, dgb, dbb;
   const float *gbp = nullptr, *mbp = nullptr, *ibp = nullptr;
   if (nsets == 2) {
     coef_b = torch::empty({3, C}, fo);
-    dgb = torch::empty({C}, fo);
-    dbb = torch::empty({C}, fo);
+    dgb = sinks ? *sink_gb : torch::empty({C}, fo);
+    dbb = sinks ? *sink_bb : torch::empty({C}, fo);
+    if (sinks) {
+      check_vec(dgb, C, "sink_gb");
+      check_vec(dbb, C, "sink_bb");
+    }
     gbp = opt_ptr(g_b, C, "g_b");
     mbp = opt_ptr(mean_b, C, "mean_b");
     ibp = opt_ptr(inv_b, C, "inv_b");
@@ -261,7 +333,7 @@ std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_
                                coef_a.data_ptr<float>(), nsets == 2 ? coef_b.data_ptr<float>() : nullptr,
                                dga.data_ptr<float>(), dba.data_ptr<float>(),
                                nsets == 2 ? dgb.data_ptr<float>() : nullptr,
-                               nsets == 2 ? dbb.data_ptr<float>() : nullptr, cur_stream()),
+                               nsets == 2 ? dbb.data_ptr<float>() : nullptr, sinks ? 1 : 0, cur_stream()),
             "bn_bwd_coef");
   return {coef_a, coef_b, dga, dba, dgb, dbb};
 }
@@ -306,14 +378,24 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
 
 void register_conv_bn(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16) + BN stat slab");
-  m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv data gradient");
-  m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K)");
+  m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv data gradient (strided: sub-pixel classes)",
+        pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("stride"),
+        pybind11::arg("pad"), pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("addend") = pybind11::none());
+  m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K slab)", pybind11::arg("dy"),
+        pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("stride"), pybind11::arg("pad"),
+        pybind11::arg("splits") = 0, pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("accumulate") = false);
   m.def("bn_stats_reduce", &bn_stats_reduce);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_affine", &bn_eval_affine);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
-  m.def("bn_bwd_coef", &bn_bwd_coef);
+  m.def("bn_bwd_coef", &bn_bwd_coef, pybind11::arg("sums"), pybind11::arg("count"), pybind11::arg("g_a"),
+        pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),
+        pybind11::arg("mean_b") = pybind11::none(), pybind11::arg("inv_b") = pybind11::none(),
+        pybind11::arg("sink_ga") = pybind11::none(), pybind11::arg("sink_ba") = pybind11::none(),
+        pybind11::arg("sink_gb") = pybind11::none(), pybind11::arg("sink_bb") = pybind11::none());
   m.def("bn_bwd_apply", &bn_bwd_apply);
 }
 

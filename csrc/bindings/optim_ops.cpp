@@ -50,3 +50,24 @@ void register_optim(pybind11::module& m) {
 }
 
 }  // namespace sdx_bind
+
+namespace sdx_bind {
+namespace {
+
+void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int64_t total) {
+  TORCH_CHECK(master.is_cuda() && master.scalar_type() == at::kFloat && master.is_contiguous(), "master fp32");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous(), "out bf16");
+  TORCH_CHECK(segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2 && segs.size(1) == 7 &&
+                  segs.is_contiguous(),
+              "segs int64 [nseg, 7]");
+  c10::DeviceGuard dg(master.device());
+  check_hip(launch_wprep(master.data_ptr<float>(), out.data_ptr(), segs.data_ptr(), (int)segs.size(0), total,
+                         cur_stream()),
+            "wprep");
+}
+
+}  // namespace
+
+void register_wprep(pybind11::module& m) { m.def("wprep", &wprep, "fp32 master -> bf16 fwd/dgrad conv weights"); }
+
+}  // namespace sdx_bind

@@ -7,6 +7,7 @@ void register_conv_bn(pybind11::module& m);
 void register_data(pybind11::module& m);
 void register_optim(pybind11::module& m);
 void register_pool(pybind11::module& m);
+void register_wprep(pybind11::module& m);
 
 void register_ops(pybind11::module& m) {
   register_supcon(m);
@@ -14,5 +15,6 @@ void register_ops(pybind11::module& m) {
   register_data(m);
   register_optim(m);
   register_pool(m);
+  register_wprep(m);
 }
 }  // namespace sdx_bind

@@ -54,6 +54,27 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Division by a runtime-invariant divisor via multiply-high (Granlund-Montgomery);
+// exact for 0 <= x < 2^31.
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f{d, 0u, 0u};
+  if (d > 1) {
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+    f.shr = l;
+  }
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  return (__umulhi(x, f.mul) + x) >> f.shr;
+}
+
 }  // namespace sdx
 
 #define SDX_LAUNCH_CHECK() \

@@ -32,10 +32,15 @@ int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s);
-hipError_t launch_conv_dgrad(const ConvGeom& g, const void* dy, const void* wt, void* dx, int cfg,
-                             hipStream_t s);
-hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* dw, int cfg, int splits,
-                             hipStream_t s);
+// strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous)
+void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
+// addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
+hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
+                                   const void* addend, int cfg, hipStream_t s);
+int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
+// partial: fp32 [splits][K][R*S*C] workspace (unused when splits == 1 and !accumulate)
+hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,
+                             int splits, int accumulate, hipStream_t s);
 
 // ---- BatchNorm (bn.hip) ---------------------------------------------------------
 hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s);
@@ -52,7 +57,7 @@ hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* 
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
                               const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
                               const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
-                              float* dgamma_b, float* dbeta_b, hipStream_t s);
+                              float* dgamma_b, float* dbeta_b, int accumulate, hipStream_t s);
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
                                const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s);
 
@@ -77,3 +82,7 @@ hipError_t launch_maxpool_bwd(const void* x, const void* y, const void* dy, void
                               int P, int Q, int k, int stride, int pad, hipStream_t s);
 hipError_t launch_gap_fwd(const void* x, float* y, int N, int HW, int C, hipStream_t s);
 hipError_t launch_gap_bwd(const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
+
+// ---- weight preparation (wprep.hip) ---------------------------------------------
+// segs: device table of nseg rows {src, dst_k, dst_t, K|RS<<32, C|Cp<<32, n, start} (int64)
+hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s);

@@ -209,7 +209,7 @@ __global__ void bn_bwd_coef_kernel(const double* __restrict__ sums, int nsets, i
                                    const float* __restrict__ mean_b, const float* __restrict__ inv_b,
                                    float* __restrict__ coef_a, float* __restrict__ coef_b,
                                    float* __restrict__ dgamma_a, float* __restrict__ dbeta_a,
-                                   float* __restrict__ dgamma_b, float* __restrict__ dbeta_b) {
+                                   float* __restrict__ dgamma_b, float* __restrict__ dbeta_b, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double sdz = sums[c];
@@ -229,8 +229,8 @@ __global__ void bn_bwd_coef_kernel(const double* __restrict__ sums, int nsets, i
     coef[2 * C + c] = (float)E;
     float* dg = set == 0 ? dgamma_a : dgamma_b;
     float* db = set == 0 ? dbeta_a : dbeta_b;
-    if (dg) dg[c] = (float)(sdzy * inv);
-    if (db) db[c] = (float)sdz;
+    if (dg) dg[c] = (float)(sdzy * inv) + (accumulate ? dg[c] : 0.f);
+    if (db) db[c] = (float)sdz + (accumulate ? db[c] : 0.f);
   }
 }
 
@@ -353,9 +353,9 @@ hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* 
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
                               const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
                               const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
-                              float* dgamma_b, float* dbeta_b, hipStream_t s) {
+                              float* dgamma_b, float* dbeta_b, int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, nsets, C, count, g_a, mean_a,
-                     inv_a, g_b, mean_b, inv_b, coef_a, coef_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b);
+                     inv_a, g_b, mean_b, inv_b, coef_a, coef_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b, accumulate);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

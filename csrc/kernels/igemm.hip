@@ -3,24 +3,30 @@
 // One kernel template implements the three convolution GEMMs of training
 // (reference model: networks/resnet_big.py:38-118, every nn.Conv2d of the encoder):
 //
-//   FWD   y[m=(n,p,q)][co]        = Σ_{k=(r,s,ci)} x[n][p·st−pad+r][q·st−pad+s][ci] · W[co][r][s][ci]
-//   DGRAD dx[m=(n,h,w)][ci]       = Σ_{k=(r,s,co)} dy[n][(h+pad−r)/st][(w+pad−s)/st][co] · Wt[ci][r][s][co]
-//   WGRAD dW[co][j=(r,s,ci)]     += Σ_{kk=(n,p,q)} dy[kk][co] · x[n][p·st−pad+r][q·st−pad+s][ci]   (split-K)
+//   FWD   y[m=(n,p,q)][co]    = Σ_{k=(r,s,ci)} x[n][p·st−pad+r][q·st−pad+s][ci] · W[co][r][s][ci]
+//   DGRAD dx[m=(n,h,w)][ci]   = Σ_{k=(r,s,co)} dy[n][(h+pad−r)/st][(w+pad−s)/st][co] · Wt[ci][r][s][co]
+//   WGRAD dW[co][j=(r,s,ci)]  = Σ_{kk=(n,p,q)} dy[kk][co] · x[n][p·st−pad+r][q·st−pad+s][ci]   (split-K)
 //
-// Tiles: BM x BN output per 256-thread workgroup (4 waves, each a 64x64 sub-tile of
-// 4x4 v_mfma_f32_16x16x32_bf16 accumulators), BK = 64. Operands are register-staged
-// (16-byte global loads, im2col gather with zero padding done in the address
-// computation) into a double-buffered LDS image: the next K-tile's global loads are
-// issued before the current tile's MFMAs and written to the other LDS buffer after them
-// (one barrier per K-tile). "K-inner" images ([rows][64] bf16, 128-B rows, XOR-swizzled
-// by row) are read with ds_read_b128; "K-outer" images ([64][cols], used by WGRAD whose
-// operands are both strided along K) are read with ds_read_b64_tr_b16 transposed reads.
+// Strided DGRAD is decomposed into st² sub-pixel classes (h ≡ ph, w ≡ pw mod st): within
+// a class only the taps r ≡ ph+pad (mod st) contribute and (h+pad−r)/st is exact, so every
+// MFMA does useful work (a plain masked gather wastes 3/4 of it at stride 2).
 //
-// Epilogues: FWD stores bf16 y through an LDS transpose (coalesced 16-B row stores) and
-// emits per-channel BatchNorm statistics of the stored values (per-tile Σy and Σy², one
-// slab row per M-tile, reduced in fp64 by bn_stats_reduce — no atomics here);
-// DGRAD stores bf16 dx; WGRAD adds fp32 partial sums into dW with atomics.
-// Block→tile order is XCD-aware (all N-tiles of one M-tile on one XCD's L2).
+// Tiles: BM x BN output per 256-thread workgroup (4 waves, each a 64x64 sub-tile of 4x4
+// v_mfma_f32_16x16x32_bf16 accumulators), BK = 64. Operands are register-staged (16-byte
+// global loads, im2col gather + zero padding in 32-bit address math, k decoded
+// incrementally) into a double-buffered LDS image: the next K-tile's loads are issued
+// before the current tile's MFMAs and written to the other buffer after them (one barrier
+// per K-tile). "K-inner" images ([rows][64] bf16, XOR-swizzled 128-B rows) are read with
+// ds_read_b128; "K-outer" images ([64][cols], WGRAD, both operands strided along K) with
+// ds_read_b64_tr_b16 transposed reads.
+//
+// The MFMA is issued as D = Bᵀ·Aᵀ, so each lane's accumulator holds FOUR CONSECUTIVE OUTPUT
+// COLUMNS of one output row: the epilogues write 8-byte (bf16) / 16-byte (fp32) pieces.
+// FWD/DGRAD store bf16 through an LDS-staged tile as whole 16-B row chunks (optionally to
+// remapped rows: DGRAD sub-pixel classes); FWD also emits per-channel BatchNorm statistics
+// (per-M-tile Σy, Σy² of the stored values → one slab row, reduced in fp64 by
+// bn_stats_reduce). WGRAD writes an fp32 partial slab per K-split (deterministic; reduced
+// by igemm_splitk_reduce), never atomics. Block→tile order is XCD-aware.
 #include "common.h"
 #include "launchers.h"
 
@@ -34,11 +40,15 @@ constexpr int BK = 64;
 struct IgemmParams {
   ConvGeom g;
   const uint16_t* a;   // FWD: x, DGRAD: dy, WGRAD: dy
-  const uint16_t* b;   // FWD: W [K][R][S][C], DGRAD: Wt [C][R][S][K], WGRAD: x
-  void* out;           // FWD/DGRAD: bf16 [M][Ncol]; WGRAD: fp32 [K][R*S*C]
+  const uint16_t* b;   // FWD: W [K][R][S][C], DGRAD: class taps of Wt [C][nr][ns][K], WGRAD: x
+  void* out;           // FWD/DGRAD: bf16 rows of Ncol; WGRAD: fp32 partial slab [splits][M][Ncol]
   float* stats;        // FWD: [m_tiles][2][Ncol] (Σy, Σy²) or nullptr
+  const uint16_t* addend;   // DGRAD: optional bf16 tensor (same layout as out) added in the epilogue
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
+  // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
+  int ph, pw, Hc, Wc, r0, s0, nr, ns;
+  FastDiv div_pq, div_q;   // WGRAD pixel decode
 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -72,11 +82,12 @@ struct Tile {
   static constexpr int B_CH = BN * BK / 8 / 256;
 };
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   using T = Tile<MODE, BM, BN>;
-  constexpr int WM = BM / 64, WN = BN / 64;
-  static_assert(WM * WN == 4, "4 waves of 64x64");
+  constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   constexpr int LDS = 2 * T::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
@@ -97,30 +108,56 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     k_begin = split * p.k_per_split;
     k_end = min(p.Kdim, k_begin + p.k_per_split);
   }
-  const int nk = (k_end - k_begin + BK - 1) / BK;
+  const int nk = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
 
-  // ---- per-thread loader state ----
+  // ---- per-thread loader state (32-bit address math: tensors < 2^31 elements) ----
   // K-inner operands: thread owns chunk column ch = tid % 8 and rows tid/8 + 32*i.
   const int kin_ch = tid & 7;
   const int kin_row0 = tid >> 3;
-  // FWD/DGRAD A gather rows
-  int a_n[T::A_CH], a_y[T::A_CH], a_x[T::A_CH];
+  const bool is1x1 = (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
+  // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
+  // tap; DGRAD: dy coordinate of tap (r0, s0))
+  int a_base[T::A_CH], a_y[T::A_CH], a_x[T::A_CH];
+  int b_off[T::B_CH];
+  // k decode of this thread's chunk: k = kc + cdim*(ks + ns*kr)
+  int kc = 0, ks = 0, kr = 0;
+  const int cdim = (MODE == MODE_FWD) ? g.C : g.K;
+  const int tap_s = (MODE == MODE_DGRAD) ? p.ns : g.S;
   if (MODE != MODE_WGRAD) {
-    const int hw_out = (MODE == MODE_FWD) ? g.P * g.Q : g.H * g.W;
-    const int wdim = (MODE == MODE_FWD) ? g.Q : g.W;
+    const int hw_out = (MODE == MODE_FWD) ? g.P * g.Q : p.Hc * p.Wc;
+    const int wdim = (MODE == MODE_FWD) ? g.Q : p.Wc;
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
       const int m = m0 + kin_row0 + 32 * i;
       if (m < p.M) {
         const int n = m / hw_out, rem = m - n * hw_out;
         const int yy = rem / wdim, xx = rem - yy * wdim;
-        a_n[i] = n;
-        if (MODE == MODE_FWD) { a_y[i] = yy * g.stride - g.pad; a_x[i] = xx * g.stride - g.pad; }
-        else { a_y[i] = yy + g.pad; a_x[i] = xx + g.pad; }
+        if (MODE == MODE_FWD) {
+          a_y[i] = yy * g.stride - g.pad;
+          a_x[i] = xx * g.stride - g.pad;
+          a_base[i] = ((n * g.H + a_y[i]) * g.W + a_x[i]) * g.C;
+        } else {
+          // (h + pad − r0) is a multiple of st by construction of the class
+          a_y[i] = (yy * g.stride + p.ph + g.pad - p.r0) / g.stride;
+          a_x[i] = (xx * g.stride + p.pw + g.pad - p.s0) / g.stride;
+          a_base[i] = n * g.P * g.Q * g.K;
+        }
       } else {
-        a_n[i] = -1; a_y[i] = 0; a_x[i] = 0;
+        a_y[i] = -(1 << 28);   // fails every bounds test
+        a_x[i] = -(1 << 28);
+        a_base[i] = 0;
       }
     }
+#pragma unroll
+    for (int i = 0; i < T::B_CH; ++i) {
+      const int col = n0 + kin_row0 + 32 * i;
+      b_off[i] = col < p.Ncol ? col * p.Kdim : -1;
+    }
+    const int k = k_begin + kin_ch * 8;
+    kc = k % cdim;
+    const int rs = k / cdim;
+    kr = rs / tap_s;
+    ks = rs - kr * tap_s;
   }
   // WGRAD: K-outer images. A: [BK pixels][BM couts], B: [BK pixels][BN (r,s,ci)].
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;  // chunks per row
@@ -140,33 +177,25 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
 
   auto load_tile = [&](int k0) {
     if (MODE == MODE_FWD || MODE == MODE_DGRAD) {
-      // A: gather 8 consecutive k (same (r,s), 8 channels) for each owned row
+      // A: gather 8 consecutive k (same tap, 8 channels) for each owned row
       const int k = k0 + kin_ch * 8;
-      const int cdim = (MODE == MODE_FWD) ? g.C : g.K;
       const bool kok = k < k_end;
-      const int cc = k % cdim;
-      const int rs = k / cdim;
-      const int r = rs / g.S, s = rs - (rs / g.S) * g.S;
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (kok && a_n[i] >= 0) {
+        if (kok) {
           if (MODE == MODE_FWD) {
-            const int yy = a_y[i] + r, xx = a_x[i] + s;
-            if (yy >= 0 && yy < g.H && xx >= 0 && xx < g.W)
-              v = ld16(p.a + (((size_t)a_n[i] * g.H + yy) * g.W + xx) * g.C + cc);
-          } else {
-            int ty = a_y[i] - r, tx = a_x[i] - s;
-            if (ty >= 0 && tx >= 0) {
-              bool ok = true;
-              if (g.stride != 1) {
-                ok = (ty % g.stride == 0) && (tx % g.stride == 0);
-                ty /= g.stride;
-                tx /= g.stride;
-              }
-              if (ok && ty < g.P && tx < g.Q)
-                v = ld16(p.a + (((size_t)a_n[i] * g.P + ty) * g.Q + tx) * g.K + cc);
+            if (is1x1) {
+              if (a_y[i] >= 0) v = ld16(p.a + a_base[i] + kc);
+            } else {
+              const int yy = a_y[i] + kr, xx = a_x[i] + ks;
+              if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W)
+                v = ld16(p.a + a_base[i] + (kr * g.W + ks) * g.C + kc);
             }
+          } else {
+            const int ty = a_y[i] - kr, tx = a_x[i] - ks;
+            if ((unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q)
+              v = ld16(p.a + a_base[i] + (ty * g.Q + tx) * g.K + kc);
           }
         }
         ra[i] = v;
@@ -174,10 +203,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
       // B: weights [Ncol][Kdim] K-contiguous
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        const int col = n0 + kin_row0 + 32 * i;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (kok && col < p.Ncol) v = ld16(p.b + (size_t)col * p.Kdim + k);
+        if (kok && b_off[i] >= 0) v = ld16(p.b + b_off[i] + k);
         rb[i] = v;
+      }
+      // advance the k decode by one tile
+      kc += BK;
+      while (kc >= cdim) {
+        kc -= cdim;
+        if (++ks == tap_s) { ks = 0; ++kr; }
       }
     } else {
       // WGRAD A: dy rows (pixels) x BM couts
@@ -187,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         const int row = e / A_CPR, ch = e % A_CPR;
         const int kk = k0 + row, co = m0 + ch * 8;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (kk < k_end && co < p.M) v = ld16(p.a + (size_t)kk * g.K + co);
+        if (kk < k_end && co < p.M) v = ld16(p.a + kk * g.K + co);
         ra[i] = v;
       }
       // WGRAD B: im2col(x) rows (pixels) x BN (r,s,ci); the column chunk is fixed per thread
@@ -198,12 +232,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         const int kk = k0 + row;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (wb_ok && kk < k_end) {
-          const int pq = g.P * g.Q;
-          const int n = kk / pq, rem = kk - n * pq;
-          const int pp = rem / g.Q, qq = rem - pp * g.Q;
-          const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
-          if (yy >= 0 && yy < g.H && xx >= 0 && xx < g.W)
-            v = ld16(p.b + (((size_t)n * g.H + yy) * g.W + xx) * g.C + wb_c);
+          if (is1x1) {
+            v = ld16(p.b + kk * g.C + wb_c);
+          } else {
+            const int n = (int)fdiv((unsigned)kk, p.div_pq);
+            const int rem = kk - n * g.P * g.Q;
+            const int pp = (int)fdiv((unsigned)rem, p.div_q);
+            const int qq = rem - pp * g.Q;
+            const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
+            if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W)
+              v = ld16(p.b + ((n * g.H + yy) * g.W + xx) * g.C + wb_c);
+          }
         }
         rb[i] = v;
       }
@@ -234,13 +273,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment readers
+  // fragment readers: lane (h, c) gets row/col c of the 16-wide tile, k = 8h..8h+7 of step u
   auto frag_kin = [&](const unsigned char* img, int row, int u) -> bf16x8 {
     return *reinterpret_cast<const bf16x8*>(img + kin_off(row, 4 * u + h));
   };
@@ -273,66 +312,64 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     const unsigned char* sb = sa + T::A_BYTES;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (T::A_KIN) af[i] = frag_kin(sa, wm * 64 + 16 * i + c, u);
-        else af[i] = frag_kout(sa, wm * 64 + 16 * i, u, std::integral_constant<int, BM>{});
+      for (int i = 0; i < TM; ++i) {
+        if (T::A_KIN) af[i] = frag_kin(sa, wm * WTM + 16 * i + c, u);
+        else af[i] = frag_kout(sa, wm * WTM + 16 * i, u, std::integral_constant<int, BM>{});
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (T::B_KIN) bfr[j] = frag_kin(sb, wn * 64 + 16 * j + c, u);
-        else bfr[j] = frag_kout(sb, wn * 64 + 16 * j, u, std::integral_constant<int, BN>{});
+      for (int j = 0; j < TN; ++j) {
+        if (T::B_KIN) bfr[j] = frag_kin(sb, wn * WTN + 16 * j + c, u);
+        else bfr[j] = frag_kout(sb, wn * WTN + 16 * j, u, std::integral_constant<int, BN>{});
       }
+      // D = Bᵀ·Aᵀ: accumulator column = output row (lane c), rows = output columns (4h + r)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (more) store_tile(buf ^ 1);
     __syncthreads();
   }
 
   // ---------------------------------- epilogues ----------------------------------
-  // acc[i][j][r] = C[m0 + wm*64 + 16i + 4h + r][n0 + wn*64 + 16j + c]
+  // acc[i][j][r] = C[m0 + wm*64 + 16i + c][n0 + wn*64 + 16j + 4h + r]
   if (MODE == MODE_WGRAD) {
-    float* out = reinterpret_cast<float*>(p.out);
+    float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.Ncol;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + wm * WTM + 16 * i + c;
+      if (row >= p.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + 16 * j + c;
-        if (col >= p.Ncol) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 64 + 16 * i + 4 * h + r;
-          if (row < p.M) atomicAdd(out + (size_t)row * p.Ncol + col, acc[i][j][r]);
-        }
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WTN + 16 * j + 4 * h;
+        if (col < p.Ncol)
+          *reinterpret_cast<float4*>(out + (size_t)row * p.Ncol + col) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
+    }
     return;
   }
 
-  // bf16 rounding (stats describe the stored tensor)
-  uint16_t ov[4][4][4];
+  // bf16 rounding (stats describe the stored tensor); pack 4 consecutive columns
+  uint2 ov[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ov[i][j][r] = f2bf(acc[i][j][r]);
+    for (int j = 0; j < TN; ++j)
+      ov[i][j] = make_uint2(pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3]));
 
-  // stage the C tile through LDS ([BM][BN] bf16, padded rows) for coalesced stores
-  constexpr int CRS = BN * 2 + 16;
+  // stage the C tile through LDS ([BM][BN] bf16, rows padded by 8 B: 16 lanes writing 8 B
+  // at the same column of 16 consecutive rows hit distinct banks)
+  constexpr int CRS = BN * 2 + 8;
   static_assert(BM * CRS <= LDS, "C tile must fit the staging LDS");
-  uint16_t* ctile = reinterpret_cast<uint16_t*>(smem);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ctile[((wm * 64 + 16 * i + 4 * h + r) * CRS) / 2 + wn * 64 + 16 * j + c] = ov[i][j][r];
+    for (int j = 0; j < TN; ++j)
+      *reinterpret_cast<uint2*>(smem + (wm * WTM + 16 * i + c) * CRS + (wn * WTN + 16 * j + 4 * h) * 2) = ov[i][j];
   __syncthreads();
   {
     uint16_t* out = reinterpret_cast<uint16_t*>(p.out);
@@ -341,38 +378,74 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
       const int row = e / CPR, ch = e % CPR;
       const int m = m0 + row, col = n0 + ch * 8;
       if (m < p.M && col < p.Ncol) {
-        const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const unsigned char*>(ctile) + row * CRS + ch * 16);
-        *reinterpret_cast<uint4*>(out + (size_t)m * p.Ncol + col) = v;
+        const unsigned char* src = smem + row * CRS + ch * 16;
+        const uint2 lo = *reinterpret_cast<const uint2*>(src);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + 8);
+        int orow = m;
+        if (MODE == MODE_DGRAD && g.stride != 1) {
+          const int hw = p.Hc * p.Wc;
+          const int n = m / hw, rem = m - n * hw;
+          const int yy = rem / p.Wc, xx = rem - yy * p.Wc;
+          orow = (n * g.H + yy * g.stride + p.ph) * g.W + xx * g.stride + p.pw;
+        }
+        uint4 v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        if (MODE == MODE_DGRAD && p.addend != nullptr) {
+          // fused residual-gradient accumulation: out = dgrad + addend (may alias out)
+          const uint4 a = *reinterpret_cast<const uint4*>(p.addend + (size_t)orow * p.Ncol + col);
+          const uint32_t* vw = reinterpret_cast<const uint32_t*>(&v);
+          const uint32_t* aw = reinterpret_cast<const uint32_t*>(&a);
+          uint32_t r[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float x0 = __uint_as_float(vw[q] << 16) + __uint_as_float(aw[q] << 16);
+            const float x1 = __uint_as_float(vw[q] & 0xffff0000u) + __uint_as_float(aw[q] & 0xffff0000u);
+            r[q] = pack_bf2(x0, x1);
+          }
+          v = make_uint4(r[0], r[1], r[2], r[3]);
+        }
+        *reinterpret_cast<uint4*>(out + (size_t)orow * p.Ncol + col) = v;
       }
     }
   }
 
   if (MODE == MODE_FWD && p.stats != nullptr) {
-    // per-column (Σy, Σy²) over this tile's valid rows, from the rounded (stored) values;
-    // one slab row per M-tile, reduced in fp64 by bn_stats_reduce (no atomics here).
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);   // [WM][2][BN]
-    const int valid_rows = min(BM, p.M - m0);
+    // per-column (Σy, Σy²) over this tile's rows (rows past M are exact zeros: their A rows
+    // were zero-filled), from the rounded values; one slab row per M-tile.
+    float s1[TN][4], s2[TN][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int r = 0; r < 4; ++r) {
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const uint32_t w = (r < 2) ? ov[i][j].x : ov[i][j].y;
+          const float v = __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+          a1 += v;
+          a2 += v * v;
+        }
+        s1[j][r] = a1;
+        s2[j][r] = a2;
+      }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = wm * 64 + 16 * i + 4 * h + r;
-          const float v = (row < valid_rows) ? bf2f(ov[i][j][r]) : 0.f;
-          s1 += v;
-          s2 += v * v;
+          s1[j][r] += __shfl_xor(s1[j][r], off, 64);
+          s2[j][r] += __shfl_xor(s2[j][r], off, 64);
         }
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (h == 0) {
-        red[(wm * 2 + 0) * BN + wn * 64 + 16 * j + c] = s1;
-        red[(wm * 2 + 1) * BN + wn * 64 + 16 * j + c] = s2;
-      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);   // [WM][2][BN]
+    if (c == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          red[(wm * 2 + 0) * BN + wn * WTN + 16 * j + 4 * h + r] = s1[j][r];
+          red[(wm * 2 + 1) * BN + wn * WTN + 16 * j + 4 * h + r] = s2[j][r];
+        }
     }
     __syncthreads();
     for (int e = tid; e < 2 * BN; e += 256) {
@@ -385,22 +458,63 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   }
 }
 
-template <int MODE, int BM, int BN>
+// dW = Σ_split partial[split] (fp32); optional accumulate into dW. A block owns 64 float4
+// columns; its 4 thread rows sum interleaved splits with 4 independent accumulators each
+// (many loads in flight), then combine through LDS — deterministic order.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, long n4,
+                                                            float* __restrict__ out, int accumulate) {
+  __shared__ float4 red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + tx;
+  const float4* P = reinterpret_cast<const float4*>(part);
+  float4 a[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n4) {
+    int k = ty;
+    for (; k + 12 < splits; k += 16) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = P[(size_t)(k + 4 * q) * n4 + e];
+        a[q].x += v.x; a[q].y += v.y; a[q].z += v.z; a[q].w += v.w;
+      }
+    }
+    for (; k < splits; k += 4) {
+      const float4 v = P[(size_t)k * n4 + e];
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
+  }
+  float4 s = a[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q) { s.x += a[q].x; s.y += a[q].y; s.z += a[q].z; s.w += a[q].w; }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && e < n4) {
+    float4 t = accumulate ? reinterpret_cast<const float4*>(out)[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { t.x += red[q][tx].x; t.y += red[q][tx].y; t.z += red[q][tx].z; t.w += red[q][tx].w; }
+    reinterpret_cast<float4*>(out)[e] = t;
+  }
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   p.m_tiles = (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
   const int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), dim3(grid), dim3(256), 0, s, p);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
 
+// tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32)
 template <int MODE>
 hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: return launch_cfg<MODE, 128, 128>(p, s);
-    case 1: return launch_cfg<MODE, 256, 64>(p, s);
-    case 2: return launch_cfg<MODE, 64, 256>(p, s);
+    case 0: return launch_cfg<MODE, 128, 128, 2, 2>(p, s);
+    case 1: return launch_cfg<MODE, 256, 64, 4, 1>(p, s);
+    case 2: return launch_cfg<MODE, 64, 256, 1, 4>(p, s);
+    case 3: return launch_cfg<MODE, 64, 64, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -408,7 +522,7 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
 }  // namespace
 
 int igemm_tile_m(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 256 : 64; }
-int igemm_tile_n(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 64 : 256; }
+int igemm_tile_n(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 64 : cfg == 2 ? 256 : 64; }
 
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s) {
@@ -424,26 +538,48 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
   return launch_any<MODE_FWD>(p, cfg, s);
 }
 
-hipError_t launch_conv_dgrad(const ConvGeom& g, const void* dy, const void* wt, void* dx, int cfg,
-                             hipStream_t s) {
+void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc) {
+  const int st = g.stride;
+  *r0 = (ph + g.pad) % st;
+  *s0 = (pw + g.pad) % st;
+  *nr = *r0 < g.R ? (g.R - *r0 + st - 1) / st : 0;
+  *ns = *s0 < g.S ? (g.S - *s0 + st - 1) / st : 0;
+  *Hc = ph < g.H ? (g.H - ph + st - 1) / st : 0;
+  *Wc = pw < g.W ? (g.W - pw + st - 1) / st : 0;
+}
+
+hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
+                                   const void* addend, int cfg, hipStream_t s) {
   IgemmParams p{};
   p.g = g;
   p.a = (const uint16_t*)dy;
-  p.b = (const uint16_t*)wt;
+  p.b = (const uint16_t*)wt_cls;
   p.out = dx;
-  p.M = g.N * g.H * g.W;
+  p.addend = (const uint16_t*)addend;
+  p.ph = ph;
+  p.pw = pw;
+  conv_dgrad_class(g, ph, pw, &p.r0, &p.nr, &p.s0, &p.ns, &p.Hc, &p.Wc);
+  p.M = g.N * p.Hc * p.Wc;
+  if (p.M == 0) return hipSuccess;
   p.Ncol = g.C;
-  p.Kdim = g.R * g.S * g.K;
+  p.Kdim = p.nr * p.ns * g.K;
   return launch_any<MODE_DGRAD>(p, cfg, s);
 }
 
-hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* dw, int cfg, int splits,
-                             hipStream_t s) {
+int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits) {
+  const int Kd = g.N * g.P * g.Q;
+  if (splits < 1) splits = 1;
+  int per = (Kd + splits - 1) / splits;
+  per = ((per + BK - 1) / BK) * BK;
+  return (Kd + per - 1) / per;
+}
+
+hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,
+                             int splits, int accumulate, hipStream_t s) {
   IgemmParams p{};
   p.g = g;
   p.a = (const uint16_t*)dy;
   p.b = (const uint16_t*)x;
-  p.out = dw;
   p.M = g.K;
   p.Ncol = g.R * g.S * g.C;
   p.Kdim = g.N * g.P * g.Q;
@@ -452,5 +588,16 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
   per = ((per + BK - 1) / BK) * BK;
   p.k_per_split = per;
   p.splits = (p.Kdim + per - 1) / per;
-  return launch_any<MODE_WGRAD>(p, cfg, s);
+  p.div_pq = make_fastdiv((unsigned)(g.P * g.Q));
+  p.div_q = make_fastdiv((unsigned)g.Q);
+  // a single split writes straight into dW (unless accumulating)
+  const bool direct = p.splits == 1 && !accumulate;
+  p.out = direct ? (void*)dw : (void*)partial;
+  hipError_t e = launch_any<MODE_WGRAD>(p, cfg, s);
+  if (e != hipSuccess || direct) return e;
+  const long n4 = (long)p.M * p.Ncol / 4;
+  const long grid = (n4 + 63) / 64;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, partial, p.splits, n4, dw, accumulate);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
 }

@@ -46,11 +46,11 @@ from . import checkpoint as ckpt_mod
 def resolve_backend(requested: str, device: torch.device, stem: str = "cifar") -> str:
     if requested == "torch":
         return "torch"
-    native_ok = device.type == "cuda" and _ext.available() and stem == "cifar"
+    native_ok = device.type == "cuda" and _ext.available()
     if requested == "native":
         if not native_ok:
             _ext.require()
-            raise RuntimeError("native backend needs a GPU and the CIFAR stem")
+            raise RuntimeError("native backend needs a GPU")
         return "native"
     return "native" if native_ok else "torch"
 
@@ -95,7 +95,7 @@ class PretrainEngine:
                                          opt.weight_decay, backend="torch" if self.backend == "torch" else "auto")
         self.reducer = GradBucketReducer(self.flat) if world > 1 else None
         self.optimizer.grad_scale = (1.0 / world) if opt.grad_semantics == "ref" else 1.0
-        self.runner = ModelRunner(model, self.backend, opt.precision, self.sync_group)
+        self.runner = ModelRunner(model, self.backend, opt.precision, self.sync_group, master=self.flat.flat)
         self.criterion = DistributedContrastiveLoss(opt.method, opt.temp, opt.base_temperature, opt.contrast_mode,
                                                     backend="native" if self.backend == "native" else "torch")
         # data: whole uint8 dataset resident on the device

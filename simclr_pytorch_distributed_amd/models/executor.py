@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from ..ops.bn import bn_act, bn_add_act
 from ..ops.conv import conv2d_nhwc
+from ..ops.pool import global_avgpool_nhwc, maxpool_nhwc
 from .resnet import BasicBlock, Bottleneck, ResNet
 
 INPUT_CHANNELS_PADDED = 8   # NHWC input images carry 3 channels padded to 8 (16-byte rows)
@@ -52,18 +53,20 @@ def _basic(b: BasicBlock, x, training, group):
 
 def encoder_forward_native(enc: ResNet, x_nhwc: torch.Tensor, training: bool = True, group=None) -> torch.Tensor:
     """``x_nhwc``: [N, H, W, 8] bf16 (3 real channels). Returns fp32 [N, feat_dim]."""
-    if enc.stem != "cifar":
-        raise NotImplementedError("native path: ImageNet stem (7x7/2 + maxpool) not implemented yet")
     cin = enc.conv1.weight.shape[1]
     pad_c = x_nhwc.shape[-1] - cin
-    y, s = conv2d_nhwc(x_nhwc, enc.conv1.weight, 1, 1, training, cin_pad=pad_c)
-    out = bn_act(y, s, enc.bn1, True, training, group)
+    if enc.stem == "cifar":      # 3x3/1, no max-pool (networks/resnet_big.py:75)
+        y, s = conv2d_nhwc(x_nhwc, enc.conv1.weight, 1, 1, training, cin_pad=pad_c)
+        out = bn_act(y, s, enc.bn1, True, training, group)
+    else:                        # ImageNet stem: 7x7/2 conv + 3x3/2 max-pool
+        y, s = conv2d_nhwc(x_nhwc, enc.conv1.weight, 2, 3, training, cin_pad=pad_c)
+        out = maxpool_nhwc(bn_act(y, s, enc.bn1, True, training, group), 3, 2, 1)
     for blk in enc.blocks():
         if isinstance(blk, Bottleneck):
             out = _bottleneck(blk, out, training, group)
         else:
             out = _basic(blk, out, training, group)
-    return out.float().mean(dim=(1, 2))
+    return global_avgpool_nhwc(out)
 
 
 def head_forward(head, feat: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
@@ -91,16 +94,47 @@ class ModelRunner:
     NCHW float images for ``torch`` and NHWC bf16 (C padded to 8) for ``native``.
     """
 
-    def __init__(self, model, backend: str = "native", precision: str = "bf16", sync_group=None):
+    def __init__(self, model, backend: str = "native", precision: str = "bf16", sync_group=None,
+                 master: torch.Tensor = None, fused: bool = True):
         self.model = model
         self.backend = backend
         self.precision = precision
         self.sync_group = sync_group
+        self.master = master
+        self.fused = fused
+        self._wc = None
+        self._nbt = None
+
+    def weight_cache(self):
+        if self._wc is None:
+            from ..ops.weights import ConvWeightCache
+            enc = self.model.encoder
+            convs = [m for m in enc.modules() if isinstance(m, torch.nn.Conv2d)]
+            self._wc = ConvWeightCache(convs, self.master, {id(enc.conv1): INPUT_CHANNELS_PADDED})
+            self._nbt = [m.num_batches_tracked for m in enc.modules()
+                         if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
+        return self._wc
+
+    def _encode_fused(self, x, training):
+        from ..ops import block as fb
+        enc = self.model.encoder
+        wc = self.weight_cache()
+        wc.refresh()
+        g = self.sync_group
+        out = fb.stem(x, enc, wc, training, g)
+        for blk in enc.blocks():
+            out = fb.bottleneck(out, blk, wc, training, g) if isinstance(blk, Bottleneck) else \
+                fb.basic(out, blk, wc, training, g)
+        if training and self._nbt:
+            torch._foreach_add_(self._nbt, 1)
+        return global_avgpool_nhwc(out)
 
     def encode(self, x, training=None):
         enc = self.model.encoder
         training = enc.training if training is None else training
         if self.backend == "native":
+            if self.fused:
+                return self._encode_fused(x, training)
             return encoder_forward_native(enc, x, training, self.sync_group)
         if x.is_cuda and self.precision == "bf16":
             with torch.autocast("cuda", dtype=torch.bfloat16):

@@ -1,0 +1,237 @@
+"""Fused ResNet building blocks: one autograd node per Bottleneck / BasicBlock / stem.
+
+Forward and backward of a whole residual block are explicit kernel sequences (reference
+math: networks/resnet_big.py:7-67), which lets the executor
+
+* reuse one bf16 weight cache for all convs (one ``wprep`` launch per step);
+* write every parameter gradient straight into its ``.grad`` sink (conv dW through the
+  split-K reduce, BN dγ/dβ from the coefficient kernel) — no AccumulateGrad adds;
+* fuse the residual-gradient sum into the last data-gradient GEMM epilogue
+  (``dx = dgrad(conv1) + dgrad(shortcut) | + dz``) instead of a separate add pass;
+* run SyncBN as one fp64 all-reduce per BN per direction.
+
+Parameters are passed to ``apply`` only to keep the autograd graph connected (their
+returned gradients are ``None``: the sinks already hold them); the bucket reducer is
+notified through :mod:`ops.sinks`.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _ext, sinks
+
+
+def _world(group) -> int:
+    return dist.get_world_size(group) if group is not None else 1
+
+
+class _BN:
+    """Per-BN forward state: finalize (train) or eval affine."""
+
+    @staticmethod
+    def forward(m, sums, bn, count, training, group):
+        if training:
+            if group is not None:
+                dist.all_reduce(sums, group=group)
+            sc, sh, mean, inv = m.bn_finalize(sums, float(count), bn.weight.detach(), bn.bias.detach(), bn.eps,
+                                              bn.momentum if bn.momentum is not None else 0.1,
+                                              bn.track_running_stats, bn.running_mean, bn.running_var)
+            return sc, sh, mean, inv
+        sc, sh = m.bn_eval_affine(bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.eps)
+        return sc, sh, None, None
+
+
+def _conv(m, x, w, stride, pad, stats):
+    y, slab = m.conv_fwd(x, w, stride, pad, stats, -1)
+    return y, (m.bn_stats_reduce(slab) if stats else None)
+
+
+def _bn_bwd(m, dout, out, y, mean, inv, bn, count, group, y_b=None, mean_b=None, inv_b=None, bn_b=None,
+            want_dz=False):
+    """BN(+second BN)+ReLU backward with dγ/dβ written into the parameter sinks."""
+    s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b)
+    if group is not None:
+        dist.all_reduce(s, group=group)
+    if y_b is None:
+        ca, _, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv,
+                                          sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias))
+        dya, _, dz = m.bn_bwd_apply(dout, out, y, ca, None, None, want_dz)
+        return dya, None, dz
+    ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, bn_b.weight.detach(), mean_b,
+                                       inv_b, sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias),
+                                       sink_gb=sinks.target(bn_b.weight), sink_bb=sinks.target(bn_b.bias))
+    dya, dyb, _ = m.bn_bwd_apply(dout, out, y, ca, y_b, cb, False)
+    return dya, dyb, None
+
+
+def _wgrad(m, dy, x, cv, stride, pad):
+    R, S = cv.weight.shape[2], cv.weight.shape[3]
+    m.conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sinks.target(cv.weight), True)
+
+
+class _Bottleneck(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blk, wc, training, group, *params):
+        m = _ext.require()
+        proj = len(blk.shortcut) > 0
+        st = blk.stride
+        y1, s1 = _conv(m, x, wc.fwd(blk.conv1), 1, 0, training)
+        cnt1 = (y1.numel() // y1.shape[-1]) * _world(group)
+        sc1, sh1, mu1, iv1 = _BN.forward(m, s1, blk.bn1, cnt1, training, group)
+        a1 = m.bn_apply(y1, sc1, sh1, None, None, None, 0, True)
+        y2, s2 = _conv(m, a1, wc.fwd(blk.conv2), st, 1, training)
+        cnt2 = (y2.numel() // y2.shape[-1]) * _world(group)
+        sc2, sh2, mu2, iv2 = _BN.forward(m, s2, blk.bn2, cnt2, training, group)
+        a2 = m.bn_apply(y2, sc2, sh2, None, None, None, 0, True)
+        y3, s3 = _conv(m, a2, wc.fwd(blk.conv3), 1, 0, training)
+        sc3, sh3, mu3, iv3 = _BN.forward(m, s3, blk.bn3, cnt2, training, group)
+        ys = mus = ivs = None
+        if proj:
+            ys, ss = _conv(m, x, wc.fwd(blk.shortcut[0]), st, 0, training)
+            scs, shs, mus, ivs = _BN.forward(m, ss, blk.shortcut[1], cnt2, training, group)
+            out = m.bn_apply(y3, sc3, sh3, ys, scs, shs, 1, True)
+        else:
+            out = m.bn_apply(y3, sc3, sh3, x, None, None, 2, True)
+        if training:
+            ctx.save_for_backward(x, y1, a1, y2, a2, y3, ys, out, mu1, iv1, mu2, iv2, mu3, iv3, mus, ivs)
+            ctx.blk, ctx.wc, ctx.group, ctx.params = blk, wc, group, params
+            ctx.cnt = (cnt1, cnt2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        m = _ext.require()
+        x, y1, a1, y2, a2, y3, ys, out, mu1, iv1, mu2, iv2, mu3, iv3, mus, ivs = ctx.saved_tensors
+        blk, wc, group = ctx.blk, ctx.wc, ctx.group
+        cnt1, cnt2 = ctx.cnt
+        st = blk.stride
+        H, W = x.shape[1], x.shape[2]
+        dout = dout.contiguous()
+        proj = ys is not None
+        if proj:
+            dy3, dys, _ = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group, ys, mus, ivs, blk.shortcut[1])
+            dz = None
+        else:
+            dy3, _, dz = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group, want_dz=True)
+        _wgrad(m, dy3, a2, blk.conv3, 1, 0)
+        da2 = m.conv_dgrad(dy3, wc.dgrad(blk.conv3), y2.shape[1], y2.shape[2], 1, 0)
+        dy2, _, _ = _bn_bwd(m, da2, a2, y2, mu2, iv2, blk.bn2, cnt2, group)
+        _wgrad(m, dy2, a1, blk.conv2, st, 1)
+        da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), H, W, st, 1)
+        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt1, group)
+        _wgrad(m, dy1, x, blk.conv1, 1, 0)
+        if proj:
+            _wgrad(m, dys, x, blk.shortcut[0], st, 0)
+            dx = m.conv_dgrad(dys, wc.dgrad(blk.shortcut[0]), H, W, st, 0)
+            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, 1, 0, -1, dx, dx)
+        else:
+            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, 1, 0, -1, None, dz)
+        sinks.notify(ctx.params)
+        return (dx, None, None, None, None) + (None,) * len(ctx.params)
+
+
+class _Basic(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blk, wc, training, group, *params):
+        m = _ext.require()
+        proj = len(blk.shortcut) > 0
+        st = blk.stride
+        y1, s1 = _conv(m, x, wc.fwd(blk.conv1), st, 1, training)
+        cnt = (y1.numel() // y1.shape[-1]) * _world(group)
+        sc1, sh1, mu1, iv1 = _BN.forward(m, s1, blk.bn1, cnt, training, group)
+        a1 = m.bn_apply(y1, sc1, sh1, None, None, None, 0, True)
+        y2, s2 = _conv(m, a1, wc.fwd(blk.conv2), 1, 1, training)
+        sc2, sh2, mu2, iv2 = _BN.forward(m, s2, blk.bn2, cnt, training, group)
+        ys = mus = ivs = None
+        if proj:
+            ys, ss = _conv(m, x, wc.fwd(blk.shortcut[0]), st, 0, training)
+            scs, shs, mus, ivs = _BN.forward(m, ss, blk.shortcut[1], cnt, training, group)
+            out = m.bn_apply(y2, sc2, sh2, ys, scs, shs, 1, True)
+        else:
+            out = m.bn_apply(y2, sc2, sh2, x, None, None, 2, True)
+        if training:
+            ctx.save_for_backward(x, y1, a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs)
+            ctx.blk, ctx.wc, ctx.group, ctx.params, ctx.cnt = blk, wc, group, params, cnt
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        m = _ext.require()
+        x, y1, a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs = ctx.saved_tensors
+        blk, wc, group, cnt = ctx.blk, ctx.wc, ctx.group, ctx.cnt
+        st = blk.stride
+        H, W = x.shape[1], x.shape[2]
+        dout = dout.contiguous()
+        proj = ys is not None
+        if proj:
+            dy2, dys, _ = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group, ys, mus, ivs, blk.shortcut[1])
+            dz = None
+        else:
+            dy2, _, dz = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group, want_dz=True)
+        _wgrad(m, dy2, a1, blk.conv2, 1, 1)
+        da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), y1.shape[1], y1.shape[2], 1, 1)
+        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt, group)
+        _wgrad(m, dy1, x, blk.conv1, st, 1)
+        if proj:
+            _wgrad(m, dys, x, blk.shortcut[0], st, 0)
+            dx = m.conv_dgrad(dys, wc.dgrad(blk.shortcut[0]), H, W, st, 0)
+            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, st, 1, -1, dx, dx)
+        else:
+            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, st, 1, -1, None, dz)
+        sinks.notify(ctx.params)
+        return (dx, None, None, None, None) + (None,) * len(ctx.params)
+
+
+class _Stem(torch.autograd.Function):
+    """conv1 + bn1 + ReLU (+ 3x3/2 max-pool for the ImageNet stem); no input gradient."""
+
+    @staticmethod
+    def forward(ctx, x, enc, wc, training, group, *params):
+        m = _ext.require()
+        imagenet = enc.stem == "imagenet"
+        st, pad = (2, 3) if imagenet else (1, 1)
+        y, s = _conv(m, x, wc.fwd(enc.conv1), st, pad, training)
+        cnt = (y.numel() // y.shape[-1]) * _world(group)
+        sc, sh, mu, iv = _BN.forward(m, s, enc.bn1, cnt, training, group)
+        a = m.bn_apply(y, sc, sh, None, None, None, 0, True)
+        out = m.maxpool_fwd(a, 3, 2, 1) if imagenet else a
+        if training:
+            ctx.save_for_backward(x, y, a, out, mu, iv)
+            ctx.enc, ctx.group, ctx.params, ctx.cnt, ctx.geo = enc, group, params, cnt, (st, pad, imagenet)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        m = _ext.require()
+        x, y, a, out, mu, iv = ctx.saved_tensors
+        st, pad, imagenet = ctx.geo
+        dout = dout.contiguous()
+        da = m.maxpool_bwd(a, out, dout, 3, 2, 1) if imagenet else dout
+        dy, _, _ = _bn_bwd(m, da, a, y, mu, iv, ctx.enc.bn1, ctx.cnt, ctx.group)
+        w = ctx.enc.conv1.weight
+        K, C, R, S = w.shape
+        dwk = m.conv_wgrad(dy, x, R, S, st, pad, 0, -1)          # [K][R][S][Cp] fp32
+        g = sinks.target(w)
+        g.add_(dwk[..., :C].permute(0, 3, 1, 2))
+        sinks.notify(ctx.params)
+        return (None, None, None, None, None) + (None,) * len(ctx.params)
+
+
+def block_params(mod) -> List[torch.nn.Parameter]:
+    return [p for p in mod.parameters()]
+
+
+def bottleneck(x, blk, wc, training: bool, group=None):
+    return _Bottleneck.apply(x, blk, wc, training, group, *block_params(blk))
+
+
+def basic(x, blk, wc, training: bool, group=None):
+    return _Basic.apply(x, blk, wc, training, group, *block_params(blk))
+
+
+def stem(x, enc, wc, training: bool, group=None):
+    ps = [enc.conv1.weight, enc.bn1.weight, enc.bn1.bias]
+    return _Stem.apply(x, enc, wc, training, group, *ps)

@@ -53,11 +53,21 @@ class GradBucketReducer:
         self.is_cuda = flat.grad.is_cuda
         self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (self.is_cuda and self.enabled) else None
         self._hooks = []
+        self._index = {id(p): i for i, p in enumerate(flat.params)}
+        self._listener = None
         if self.enabled:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            # fused native blocks write gradients into their sinks directly and notify here
+            from ..ops import sinks
+            self._listener = sinks.add_listener(self._on_sink)
             if broadcast_init:
                 self.broadcast_parameters()
+
+    def _on_sink(self, p):
+        i = self._index.get(id(p))
+        if i is not None:
+            self._make_hook(i)(p)
 
     # ---- init ---------------------------------------------------------------------
     @torch.no_grad()
@@ -106,3 +116,7 @@ class GradBucketReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self._listener is not None:
+            from ..ops import sinks
+            sinks.remove_listener(self._listener)
+            self._listener = None

@@ -29,7 +29,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 def test_conv_fwd(gpu, shape, cfg):
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
@@ -48,7 +48,7 @@ def test_conv_fwd(gpu, shape, cfg):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 def test_conv_dgrad(gpu, shape, cfg):
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
@@ -64,7 +64,7 @@ def test_conv_dgrad(gpu, shape, cfg):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 def test_conv_wgrad(gpu, shape, cfg):
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
@@ -88,3 +88,34 @@ def test_conv_large_m(gpu):
     ref = F.conv2d(x.float(), w.float(), padding=1)
     y, _ = m.conv_fwd(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).contiguous(), 1, 1, False, -1)
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 7, 64, 64, 3, 2, 1), (3, 7, 9, 64, 128, 1, 2, 0), (2, 10, 10, 64, 64, 3, 3, 1)])
+def test_conv_dgrad_strided_odd(gpu, shape):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, W, C, K, R, st, pad = shape
+    x, w = _mk(N, H, W, C, K, R)
+    xf = x.float().requires_grad_(True)
+    out = F.conv2d(xf, w.float(), stride=st, padding=pad)
+    dy = torch.randn_like(out).bfloat16()
+    (dx_ref,) = torch.autograd.grad(out, xf, dy.float())
+    dx = m.conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), w.permute(1, 2, 3, 0).contiguous(), H, W, st, pad, -1)
+    assert _rel(dx.permute(0, 3, 1, 2), dx_ref) < 1e-2
+
+
+def test_conv_wgrad_into_sink_accumulate(gpu):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, W, C, K, R, st, pad = 4, 8, 8, 64, 128, 3, 1, 1
+    x, w = _mk(N, H, W, C, K, R)
+    wf = w.float().requires_grad_(True)
+    out = F.conv2d(x.float(), wf, stride=st, padding=pad)
+    dy = torch.randn_like(out).bfloat16()
+    (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
+    sink = torch.ones(K, C, R, R, device=gpu).contiguous(memory_format=torch.channels_last)
+    dyh, xh = dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    m.conv_wgrad(dyh, xh, R, R, st, pad, 3, -1, sink, True)
+    assert _rel(sink - 1, dw_ref) < 5e-3
+    m.conv_wgrad(dyh, xh, R, R, st, pad, 1, -1, sink, False)
+    assert _rel(sink, dw_ref) < 5e-3

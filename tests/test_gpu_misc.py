@@ -80,3 +80,28 @@ def test_native_blocks_teacher_forced(gpu):
             err = ((nat.permute(0, 3, 1, 2).float() - ref).norm() / ref.norm()).item()
             assert err < 2.5e-2, err
             r = ref
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_fused_blocks_match_unfused(gpu, name):
+    """Fused block autograd (weight cache, grad sinks, fused residual-grad) == per-op path."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    torch.manual_seed(0)
+    a = SupConResNet(name).to(gpu).to(memory_format=torch.channels_last)
+    b = SupConResNet(name).to(gpu).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    fa, fb = FlatParams(a), FlatParams(b)
+    ra = ModelRunner(a, "native", master=fa.flat, fused=True)
+    rb = ModelRunner(b, "native", master=fb.flat, fused=False)
+    x = to_nhwc_input(torch.randn(16, 3, 32, 32, device=gpu))
+    w = torch.randn(16, 128, device=gpu)
+    for r, f in ((ra, fa), (rb, fb)):
+        f.zero_grad()
+        (r.forward(x) * w).sum().backward()
+    assert torch.equal(a.encoder.layer1[0].bn1.running_mean, b.encoder.layer1[0].bn1.running_mean)
+    assert torch.equal(a.encoder.bn1.num_batches_tracked, b.encoder.bn1.num_batches_tracked)
+    ga, gb = fa.grad, fb.grad
+    rel = ((ga - gb).norm() / gb.norm()).item()
+    assert rel < 1e-3, rel
