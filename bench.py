@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--no_syncbn", action="store_true")
+    ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (single GPU)")
     a, extra = ap.parse_known_args()
 
     import torch
@@ -80,6 +81,13 @@ def main():
             torch.cuda.synchronize()
         comm.barrier()
 
+    graphed = False
+    if a.graph:
+        # capture the whole step in one hipGraph (its 2 capture warm-up steps are real steps)
+        try:
+            graphed = eng.enable_cuda_graph(next_idx(0))
+        except Exception as e:  # noqa: BLE001
+            print(f"warning: hipGraph capture failed, eager fallback: {e!r}", file=sys.stderr)
     for i in range(a.warmup):
         eng.train_step(next_idx(i), 1, i % iters, iters)
     sync()
@@ -104,7 +112,7 @@ def main():
                        "global_batch": global_batch, "per_gpu_batch": a.per_gpu_batch, "views": 2,
                        "image_size": 32, "seq_len": None,
                        "parallelism": f"dp{n}" + ("+syncbn" if n > 1 and not a.no_syncbn else ""),
-                       "backend": eng.backend, "views_per_sec": round(2 * value, 2),
+                       "backend": eng.backend, "hip_graph": graphed, "views_per_sec": round(2 * value, 2),
                        "last_loss_local": round(loss, 4)},
         }), flush=True)
     if dist.is_initialized():

@@ -65,7 +65,8 @@ hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* y
 hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, int H, int W, int S, int n_views,
                               uint64_t seed, const float* mean, const float* std, float scale_lo, float scale_hi,
                               float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
-                              float sat, float hue, float gray_p, int do_crop, int do_flip, void* out,
+                              float sat, float hue, float gray_p, int do_crop, int do_flip, const int64_t* seed_dev,
+                              void* out,
                               hipStream_t s);
 
 // ---- optimizers (optim.hip) -----------------------------------------------------

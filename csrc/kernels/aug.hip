@@ -40,6 +40,7 @@ struct AugParams {
   uint16_t* out;           // [n_views*B][S][S][8]
   int B, H, W, S, n_views;
   uint64_t seed;
+  const int64_t* seed_dev;   // optional: seed read from device memory (hipGraph replays)
   float mean[3], inv_std[3];
   float scale_lo, scale_hi, ratio_lo, ratio_hi;
   float jitter_p, bright, contrast, sat, hue, gray_p;
@@ -182,7 +183,8 @@ __global__ __launch_bounds__(256) void aug_kernel(AugParams p) {
   const int64_t src = p.idx[b];
   const uint8_t* img = p.data + (size_t)src * p.H * p.W * 3;
   if (threadIdx.x == 0) {
-    Rng rng{mix64(p.seed * 0x100000001b3ull + (uint64_t)src * 31ull + (uint64_t)view * 0x9E37ull + (uint64_t)b), 0};
+    const uint64_t seed = p.seed_dev ? (uint64_t)p.seed_dev[0] : p.seed;
+    Rng rng{mix64(seed * 0x100000001b3ull + (uint64_t)src * 31ull + (uint64_t)view * 0x9E37ull + (uint64_t)b), 0};
     make_view_params(p, rng, vp);
   }
   __syncthreads();
@@ -225,7 +227,8 @@ __global__ __launch_bounds__(256) void aug_kernel(AugParams p) {
 hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, int H, int W, int S, int n_views,
                               uint64_t seed, const float* mean, const float* std, float scale_lo, float scale_hi,
                               float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
-                              float sat, float hue, float gray_p, int do_crop, int do_flip, void* out,
+                              float sat, float hue, float gray_p, int do_crop, int do_flip, const int64_t* seed_dev,
+                              void* out,
                               hipStream_t s) {
   AugParams p{};
   p.data = data; p.idx = idx; p.out = (uint16_t*)out;
@@ -234,6 +237,7 @@ hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, in
   p.scale_lo = scale_lo; p.scale_hi = scale_hi; p.ratio_lo = ratio_lo; p.ratio_hi = ratio_hi;
   p.jitter_p = jitter_p; p.bright = bright; p.contrast = contrast; p.sat = sat; p.hue = hue; p.gray_p = gray_p;
   p.do_crop = do_crop; p.do_flip = do_flip;
+  p.seed_dev = seed_dev;
   hipLaunchKernelGGL(aug_kernel, dim3(B, n_views), dim3(256), 0, s, p);
   SDX_LAUNCH_CHECK();
   return hipSuccess;

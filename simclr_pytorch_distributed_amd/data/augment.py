@@ -73,11 +73,13 @@ class AugConfig:
                          gray_p=0.0, crop=False, flip=False, mean=mean, std=std)
 
 
-def gpu_augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed: int) -> torch.Tensor:
+def gpu_augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed, seed_t=None) -> torch.Tensor:
+    """``seed_t``: optional int64 device scalar read by the kernel at run time (graph replays)."""
     m = _ext.require()
     return m.gpu_augment(data, idx, cfg.size, cfg.n_views, int(seed) & ((1 << 63) - 1), list(cfg.mean),
                          list(cfg.std), cfg.scale[0], cfg.scale[1], cfg.ratio[0], cfg.ratio[1], cfg.jitter_p,
-                         cfg.brightness, cfg.contrast, cfg.saturation, cfg.hue, cfg.gray_p, cfg.crop, cfg.flip)
+                         cfg.brightness, cfg.contrast, cfg.saturation, cfg.hue, cfg.gray_p, cfg.crop, cfg.flip,
+                         seed_t)
 
 
 def _view_params(cfg: AugConfig, H: int, W: int, rng: _Rng):

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ..data.augment import AugConfig, augment, nhwc8_to_nchw
+from ..data.augment import gpu_augment as augment_gpu
 from ..data.datasets import build_dataset
 from ..data.sampler import DistributedIndexSampler
 from ..losses.supcon import DistributedContrastiveLoss
@@ -110,7 +111,13 @@ class PretrainEngine:
             self.logger = Logger(opt.tb_folder, flush_secs=2)
         self.start_epoch = 1
         self.global_step = 0
-        self.record_norm_mean: Optional[torch.Tensor] = None
+        # device-resident step state (so the step body is graph-capturable)
+        self.record_norm_mean = torch.zeros((), device=dev)
+        self._rnm_valid = torch.zeros((), device=dev)
+        self._seed_t = torch.zeros((1,), dtype=torch.int64, device=dev)
+        self._ramp_t = torch.zeros((), device=dev)
+        self._graph = None
+        self._graph_stats = None
         if getattr(opt, "resume", ""):
             self._resume(opt.resume)
 
@@ -124,40 +131,88 @@ class PretrainEngine:
         self.global_step = int(extra.get("global_step", 0))
         rnm = extra.get("record_norm_mean")
         if rnm is not None:
-            self.record_norm_mean = torch.tensor(float(rnm), device=self.device)
+            self.record_norm_mean.fill_(float(rnm))
+            self._rnm_valid.fill_(1.0)
         logging.info(f"resumed from {path} at epoch {self.start_epoch}")
 
     def _extra_state(self, epoch):
+        valid = float(self._rnm_valid) > 0
         return {"global_step": self.global_step, "epoch": epoch,
-                "record_norm_mean": None if self.record_norm_mean is None else float(self.record_norm_mean)}
+                "record_norm_mean": float(self.record_norm_mean) if valid else None}
 
     # ------------------------------------------------------------------------------
-    def make_views(self, idx: torch.Tensor, epoch: int, it: int) -> torch.Tensor:
-        x = augment(self.data, idx, self.aug, step_seed(self.opt.seed, epoch, it, self.rank))
-        if self.backend == "torch":
+    def make_views(self, idx: torch.Tensor, epoch: int = 1, it: int = 0) -> torch.Tensor:
+        if self.backend == "native":
+            # the seed is read from device memory by the kernel (graph-replay safe)
+            x = augment_gpu(self.data, idx, self.aug, 0, self._seed_t)
+        else:
+            x = augment(self.data, idx, self.aug, step_seed(self.opt.seed, epoch, it, self.rank))
             x = nhwc8_to_nchw(x)
         return x
 
-    def train_step(self, idx: torch.Tensor, epoch: int, it: int, iters: int):
+    def _host_prelude(self, epoch: int, it: int, iters: int):
+        """Per-step host-side scalars, written to device tensors the step body reads."""
+        opt = self.opt
+        warmup_learning_rate(opt, epoch, it, iters, self.optimizer)
+        self.optimizer._sync_lr()
+        self._seed_t.fill_(step_seed(opt.seed, epoch, it, self.rank))
+        if opt.sec or opt.l2reg:
+            now_iter = (epoch - 1) * iters + it
+            self._ramp_t.fill_(now_iter / (opt.epochs * iters))
+
+    def _step_body(self, idx: torch.Tensor, epoch: int = 1, it: int = 0):
+        """Device work of one step: no host syncs, no host-dependent control flow
+        (capturable into a hipGraph)."""
         opt = self.opt
         x = self.make_views(idx, epoch, it)
         labels = self.labels[idx]
-        warmup_learning_rate(opt, epoch, it, iters, self.optimizer)
         feats = self.runner.forward(x)
         loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
-        stats = self._norm_terms(feats, epoch, it, iters)
+        stats = self._norm_terms(feats)
         loss = loss + stats.pop("extra_loss")
         self.optimizer.zero_grad()
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish()
         self.optimizer.step()
-        self.global_step += 1
         stats["loss_local"] = loss.detach()
         return stats
 
-    def _norm_terms(self, feats, epoch, it, iters):
-        """SEC / L2-reg regularisers on un-normalised global features (main_supcon.py:295-317)."""
+    def train_step(self, idx: torch.Tensor, epoch: int, it: int, iters: int):
+        self._host_prelude(epoch, it, iters)
+        if self._graph is not None:
+            self._idx_buf.copy_(idx, non_blocking=True)
+            self._graph.replay()
+            st = self._graph_stats
+        else:
+            st = self._step_body(idx, epoch, it)
+        self.global_step += 1
+        return st
+
+    def enable_cuda_graph(self, idx_example: torch.Tensor, warmup: int = 2) -> bool:
+        """Capture the whole training step (aug → fwd → loss → bwd → SGD) in one hipGraph.
+
+        Single-process only (the data-parallel path keeps eager launches). Warm-up steps are
+        real training steps run on a side stream, as graph capture requires."""
+        if self.device.type != "cuda" or self.world > 1 or self.backend != "native":
+            return False
+        self._idx_buf = idx_example.clone()
+        self._host_prelude(1, 0, 1)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_body(self._idx_buf)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_stats = self._step_body(self._idx_buf)
+        self._graph = g
+        return True
+
+    def _norm_terms(self, feats):
+        """SEC / L2-reg regularisers on un-normalised global features (main_supcon.py:295-317).
+        The EMA ``record_norm_mean`` and the ramp live in device tensors."""
         opt = self.opt
         norms = feats.float().norm(dim=1)
         n_global = norms.numel() * self.world
@@ -170,23 +225,20 @@ class PretrainEngine:
             g = local.detach() * (self.world if self.world > 1 else 1)
         norm_mean = g[0] / n_global
         norm_var = g[1] / n_global - norm_mean * norm_mean
-        if self.record_norm_mean is None:
-            self.record_norm_mean = norm_mean.detach()
-        else:
-            m = opt.norm_momentum
-            self.record_norm_mean = (1 - m) * self.record_norm_mean + m * norm_mean.detach()
-        now_iter = (epoch - 1) * iters + it
-        ramp = now_iter / (opt.epochs * iters)
+        m = opt.norm_momentum
+        rec = self.record_norm_mean
+        rec.copy_(torch.where(self._rnm_valid > 0, (1 - m) * rec + m * norm_mean, norm_mean))
+        self._rnm_valid.fill_(1.0)
         extra = torch.zeros((), device=feats.device)
-        loss_sec = ((norms - self.record_norm_mean) ** 2).sum() / n_global
+        loss_sec = ((norms - rec) ** 2).sum() / n_global
         loss_l2 = (norms ** 2).sum() / n_global
         if opt.sec:
-            extra = extra + opt.sec_wei * ramp * loss_sec
+            extra = extra + opt.sec_wei * self._ramp_t * loss_sec
         if opt.l2reg:
-            extra = extra + opt.l2reg_wei * ramp * loss_l2
+            extra = extra + opt.l2reg_wei * self._ramp_t * loss_l2
         return {"extra_loss": extra, "norm_mean": norm_mean.detach(), "norm_var": norm_var.detach(),
                 "loss_sec": loss_sec.detach(), "loss_l2reg": loss_l2.detach(),
-                "record_norm_mean": self.record_norm_mean.detach()}
+                "record_norm_mean": rec.detach().clone()}
 
     # ------------------------------------------------------------------------------
     def train_epoch(self, epoch: int) -> float:
@@ -206,6 +258,13 @@ class PretrainEngine:
             if it >= iters:
                 break
             data_time.update(time.time() - end)
+            if opt.cuda_graph and self._graph is None and not getattr(self, "_graph_failed", False):
+                try:
+                    ok = self.enable_cuda_graph(idx)
+                    logging.info("hipGraph capture of the train step: " + ("enabled" if ok else "not applicable"))
+                except Exception as e:  # noqa: BLE001
+                    self._graph_failed = True
+                    logging.warning(f"hipGraph capture failed, running eagerly: {e!r}")
             st = self.train_step(idx, epoch, it, iters)
             loss_acc += st["loss_local"]
             window_loss += st["loss_local"]

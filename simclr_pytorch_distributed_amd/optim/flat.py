@@ -94,6 +94,8 @@ class _FlatOptimizer:
         self.steps = 0
 
     def _sync_lr(self):
+        if self.lr_t.is_cuda and torch.cuda.is_current_stream_capturing():
+            return   # the host-side lr write must stay outside a captured graph
         lr = float(self.param_groups[0]["lr"])
         if lr != self._lr_host:
             self.lr_t.fill_(lr)
