@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--no_syncbn", action="store_true")
-    ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (single GPU)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="capture the step in a hipGraph (single GPU; measured slower than eager + wgrad side stream)")
     a, extra = ap.parse_known_args()
 
     import torch

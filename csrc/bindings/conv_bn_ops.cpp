@@ -16,6 +16,24 @@ void check_bf16_nhwc(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.numel() < (1LL << 31), name, " too large for 32-bit GEMM indexing");
 }
 
+void check_vec(const torch::Tensor& t, int64_t C, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, name,
+              " must be a contiguous float32 GPU vector of length C");
+}
+
+const float* opt_ptr(const OptT& t, int64_t C, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_vec(*t, C, name);
+  return t->data_ptr<float>();
+}
+
+// fused BN+ReLU input prologue: both vectors or neither
+void in_bn_ptrs(const OptT& sc, const OptT& sh, int64_t C, const float** ps, const float** pt) {
+  *ps = opt_ptr(sc, C, "in_scale");
+  *pt = opt_ptr(sh, C, "in_shift");
+  TORCH_CHECK((*ps == nullptr) == (*pt == nullptr), "in_scale and in_shift must be given together");
+}
+
 // Pick the tile config minimising padded work, with a mild preference for the larger
 // (more MFMA-efficient) tiles: 0 128x128, 1 256x64, 2 64x256, 3 64x64.
 int auto_cfg(int64_t M, int64_t Ncol) {
@@ -32,7 +50,7 @@ int auto_cfg(int64_t M, int64_t Ncol) {
 }
 
 std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
-                                    int64_t cfg) {
+                                    int64_t cfg, OptT in_scale, OptT in_shift) {
   check_bf16_nhwc(x, "x");
   check_bf16_nhwc(w, "w");
   TORCH_CHECK(w.size(3) == x.size(3), "weight Cin != input C");
@@ -58,7 +76,10 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
   } else {
     slab = torch::empty({0}, x.options().dtype(at::kFloat));
   }
-  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream()), "conv_fwd");
+  const float *isc, *ish;
+  in_bn_ptrs(in_scale, in_shift, g.C, &isc, &ish);
+  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream(), isc, ish),
+            "conv_fwd");
   return {y, slab};
 }
 
@@ -115,7 +136,8 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
 }
 
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
-                         int64_t splits, int64_t cfg, c10::optional<torch::Tensor> out, bool accumulate) {
+                         int64_t splits, int64_t cfg, c10::optional<torch::Tensor> out, bool accumulate,
+                         OptT in_scale, OptT in_shift) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(x, "x");
   TORCH_CHECK(dy.size(0) == x.size(0), "batch mismatch");
@@ -150,24 +172,15 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     dw = torch::empty({g.K, R, S, g.C}, x.options().dtype(at::kFloat));
     accumulate = false;
   }
+  const float *isc, *ish;
+  in_bn_ptrs(in_scale, in_shift, g.C, &isc, &ish);
   torch::Tensor part;
   if (splits > 1 || accumulate)
     part = torch::empty({splits * M * Ncol}, x.options().dtype(at::kFloat));
   check_hip(launch_conv_wgrad(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
-                              dw.data_ptr<float>(), (int)cfg, (int)splits, accumulate ? 1 : 0, cur_stream()),
+                              dw.data_ptr<float>(), (int)cfg, (int)splits, accumulate ? 1 : 0, cur_stream(), isc, ish),
             "conv_wgrad");
   return dw;
-}
-
-void check_vec(const torch::Tensor& t, int64_t C, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, name,
-              " must be a contiguous float32 GPU vector of length C");
-}
-
-const float* opt_ptr(const OptT& t, int64_t C, const char* name) {
-  if (!t.has_value() || !t->defined()) return nullptr;
-  check_vec(*t, C, name);
-  return t->data_ptr<float>();
 }
 
 torch::Tensor bn_stats_reduce(torch::Tensor slab) {
@@ -255,7 +268,10 @@ void check_bwd_C(int64_t C) {
   TORCH_CHECK(C <= 2048 && (C & (C - 1)) == 0 && C >= 8, "bn backward supports power-of-two C in [8, 2048]");
 }
 
-torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb) {
+// ReLU mask: from the stored activation `outv`, or (outv None, msc/msh given) recomputed as
+// ya·msc + msh > 0 for an activation that was never materialised
+torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
+                            OptT msc, OptT msh) {
   check_bf16_nhwc(dout, "dout");
   check_bf16_nhwc(ya, "ya");
   const int64_t C = dout.size(3);
@@ -279,11 +295,13 @@ torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, tor
     mbp = mb->data_ptr<float>();
   }
   c10::DeviceGuard dg(dout.device());
+  const float *mk_s, *mk_t;
+  in_bn_ptrs(msc, msh, C, &mk_s, &mk_t);
   const int nsets = ybp ? 3 : 2;
   auto sums = torch::empty({nsets, C}, dout.options().dtype(at::kDouble));
   auto partial = torch::empty({bn_bwd_reduce_blocks(dout.numel(), C), nsets, C}, dout.options().dtype(at::kFloat));
   check_hip(launch_bn_bwd_reduce(dout.data_ptr(), op, ya.data_ptr(), ma.data_ptr<float>(), ybp, mbp, dout.numel(), C,
-                                 partial.data_ptr<float>(), sums.data_ptr<double>(), cur_stream()),
+                                 partial.data_ptr<float>(), sums.data_ptr<double>(), cur_stream(), mk_s, mk_t),
             "bn_bwd_reduce");
   return sums;
 }
@@ -339,7 +357,7 @@ std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_
 }
 
 std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ca, OptT yb,
-                                        OptT cb, bool want_dz) {
+                                        OptT cb, bool want_dz, OptT msc, OptT msh) {
   check_bf16_nhwc(dout, "dout");
   check_bf16_nhwc(ya, "ya");
   const int64_t C = dout.size(3);
@@ -366,10 +384,12 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
   } else {
     dyb = torch::empty({0}, dout.options());
   }
+  const float *mk_s, *mk_t;
+  in_bn_ptrs(msc, msh, C, &mk_s, &mk_t);
   dz = want_dz ? torch::empty_like(dout) : torch::empty({0}, dout.options());
   check_hip(launch_bn_bwd_apply(dout.data_ptr(), op, ya.data_ptr(), ca.data_ptr<float>(), ybp, cbp, dya.data_ptr(),
                                 ybp ? dyb.data_ptr() : nullptr, want_dz ? dz.data_ptr() : nullptr, dout.numel(), C,
-                                cur_stream()),
+                                cur_stream(), mk_s, mk_t),
             "bn_bwd_apply");
   return {dya, dyb, dz};
 }
@@ -377,7 +397,10 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
 }  // namespace
 
 void register_conv_bn(pybind11::module& m) {
-  m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16) + BN stat slab");
+  m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16) + BN stat slab [+ BN+ReLU prologue]",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"),
+        pybind11::arg("want_stats"), pybind11::arg("cfg") = -1, pybind11::arg("in_scale") = pybind11::none(),
+        pybind11::arg("in_shift") = pybind11::none());
   m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv data gradient (strided: sub-pixel classes)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
@@ -385,18 +408,24 @@ void register_conv_bn(pybind11::module& m) {
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K slab)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("splits") = 0, pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("accumulate") = false);
+        pybind11::arg("accumulate") = false, pybind11::arg("in_scale") = pybind11::none(),
+        pybind11::arg("in_shift") = pybind11::none());
   m.def("bn_stats_reduce", &bn_stats_reduce);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_affine", &bn_eval_affine);
   m.def("bn_apply", &bn_apply);
-  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
+        pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("mb") = pybind11::none(),
+        pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none());
   m.def("bn_bwd_coef", &bn_bwd_coef, pybind11::arg("sums"), pybind11::arg("count"), pybind11::arg("g_a"),
         pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),
         pybind11::arg("mean_b") = pybind11::none(), pybind11::arg("inv_b") = pybind11::none(),
         pybind11::arg("sink_ga") = pybind11::none(), pybind11::arg("sink_ba") = pybind11::none(),
         pybind11::arg("sink_gb") = pybind11::none(), pybind11::arg("sink_bb") = pybind11::none());
-  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bn_bwd_apply", &bn_bwd_apply, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
+        pybind11::arg("ca"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("cb") = pybind11::none(),
+        pybind11::arg("want_dz") = false, pybind11::arg("msc") = pybind11::none(),
+        pybind11::arg("msh") = pybind11::none());
 }
 
 }  // namespace sdx_bind

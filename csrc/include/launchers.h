@@ -30,8 +30,9 @@ struct ConvGeom {
 };
 int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);
+// in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
-                           hipStream_t s);
+                           hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr);
 // strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous)
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
@@ -40,7 +41,8 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
 // partial: fp32 [splits][K][R*S*C] workspace (unused when splits == 1 and !accumulate)
 hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,
-                             int splits, int accumulate, hipStream_t s);
+                             int splits, int accumulate, hipStream_t s, const float* in_scale = nullptr,
+                             const float* in_shift = nullptr);
 
 // ---- BatchNorm (bn.hip) ---------------------------------------------------------
 hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s);
@@ -53,13 +55,15 @@ hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, cons
                            const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s);
 int bn_bwd_reduce_blocks(long numel, int C);
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
-                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s);
+                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s,
+                                const float* msc = nullptr, const float* msh = nullptr);
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
                               const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
                               const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
                               float* dgamma_b, float* dbeta_b, int accumulate, hipStream_t s);
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
-                               const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s);
+                               const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s,
+                               const float* msc = nullptr, const float* msh = nullptr);
 
 // ---- GPU augmentation (aug.hip) -------------------------------------------------
 hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, int H, int W, int S, int n_views,

@@ -98,9 +98,15 @@ template <int RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ sc,
                                                        const float* __restrict__ sh, const uint16_t* __restrict__ r,
                                                        const float* __restrict__ sc2, const float* __restrict__ sh2,
-                                                       uint16_t* __restrict__ out, long n8, int C8) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n8; e += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(e % C8) * 8;
+                                                       uint16_t* __restrict__ out, long n8l, int C8) {
+  // 32-bit indexing (tensors < 2^31 elements); the channel group stays fixed per thread
+  // whenever the grid stride is a multiple of C/8 (no per-element modulo)
+  const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
+  const bool fixed = (stride % C8) == 0;
+  const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
+  int c0 = (e0 % C8) * 8;
+  for (int e = e0; e < n8; e += stride) {
+    if (!fixed) c0 = (e % C8) * 8;
     float v[8];
     unpack8(reinterpret_cast<const uint4*>(y)[e], v);
     const float4 s0 = reinterpret_cast<const float4*>(sc + c0)[0], s1 = reinterpret_cast<const float4*>(sc + c0)[1];
@@ -139,7 +145,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ outv,
                                                             const uint16_t* __restrict__ ya, const float* __restrict__ ma,
                                                             const uint16_t* __restrict__ yb, const float* __restrict__ mb,
-                                                            long n8, int C8, int C, float* __restrict__ partial) {
+                                                            long n8, int C8, int C, float* __restrict__ partial,
+                                                            const float* __restrict__ msc,
+                                                            const float* __restrict__ msh) {
   constexpr int NS = TWO ? 3 : 2;
   __shared__ float red[NS][256][8];
   const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -152,17 +160,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     mua[i] = ma[c0 + i];
     mub[i] = TWO ? mb[c0 + i] : 0.f;
   }
+  // ReLU mask recomputed from the BN input when the activation itself was never stored
+  // (its consumer applied BN+ReLU in its load prologue): out > 0  <=>  ya·msc + msh > 0
+  const bool mask_y = outv == nullptr && msc != nullptr;
+  float mks[8], mkt[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mks[i] = mask_y ? msc[c0 + i] : 0.f;
+    mkt[i] = mask_y ? msh[c0 + i] : 0.f;
+  }
   float s0[8] = {0}, s1[8] = {0}, s2[8] = {0};
   for (long e = tid; e < n8; e += stride) {
     float d[8], a[8];
     unpack8(reinterpret_cast<const uint4*>(dout)[e], d);
+    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
     if (outv) {
       float o[8];
       unpack8(reinterpret_cast<const uint4*>(outv)[e], o);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
+    } else if (mask_y) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = a[i] * mks[i] + mkt[i] > 0.f ? d[i] : 0.f;
     }
-    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       s0[i] += d[i];
@@ -240,19 +260,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            const uint16_t* __restrict__ ya, const float* __restrict__ ca,
                                                            const uint16_t* __restrict__ yb, const float* __restrict__ cb,
                                                            uint16_t* __restrict__ dya, uint16_t* __restrict__ dyb,
-                                                           uint16_t* __restrict__ dz_out, long n8, int C8, int C) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n8; e += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(e % C8) * 8;
+                                                           uint16_t* __restrict__ dz_out, long n8l, int C8, int C,
+                                                           const float* __restrict__ msc,
+                                                           const float* __restrict__ msh) {
+  const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
+  const bool fixed = (stride % C8) == 0;
+  const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
+  int c0 = (e0 % C8) * 8;
+  for (int e = e0; e < n8; e += stride) {
+    if (!fixed) c0 = (e % C8) * 8;
     float d[8], a[8], r[8];
     unpack8(reinterpret_cast<const uint4*>(dout)[e], d);
+    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
     if (outv) {
       float o[8];
       unpack8(reinterpret_cast<const uint4*>(outv)[e], o);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
+    } else if (msc) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = a[i] * msc[c0 + i] + msh[c0 + i] > 0.f ? d[i] : 0.f;
     }
     if (dz_out) reinterpret_cast<uint4*>(dz_out)[e] = pack8(d);
-    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
 #pragma unroll
     for (int i = 0; i < 8; ++i) r[i] = ca[c0 + i] * d[i] + ca[C + c0 + i] * a[i] + ca[2 * C + c0 + i];
     reinterpret_cast<uint4*>(dya)[e] = pack8(r);
@@ -333,7 +362,8 @@ int bn_bwd_reduce_blocks(long numel, int C) {
 }
 
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
-                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s) {
+                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s,
+                                const float* msc, const float* msh) {
   const int nsets = yb ? 3 : 2;
   const long n8 = numel / 8;
   const int C8 = C / 8;
@@ -341,11 +371,12 @@ hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* 
   const int g = bn_bwd_reduce_blocks(numel, C);
   if (yb)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
-                       (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)yb, mb, n8, C8, C, partial);
+                       (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)yb, mb, n8, C8, C, partial,
+                       msc, msh);
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)nullptr, (const float*)nullptr,
-                       n8, C8, C, partial);
+                       n8, C8, C, partial, msc, msh);
   SDX_LAUNCH_CHECK();
   return launch_slab_reduce(partial, g, nsets, C, sums, s);
 }
@@ -361,17 +392,18 @@ hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count
 }
 
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
-                               const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s) {
+                               const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s,
+                               const float* msc, const float* msh) {
   const long n8 = numel / 8;
   const int C8 = C / 8;
   if (yb)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)yb, cb, (uint16_t*)dya,
-                       (uint16_t*)dyb, (uint16_t*)dz_out, n8, C8, C);
+                       (uint16_t*)dyb, (uint16_t*)dz_out, n8, C8, C, msc, msh);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)nullptr, (const float*)nullptr,
-                       (uint16_t*)dya, (uint16_t*)nullptr, (uint16_t*)dz_out, n8, C8, C);
+                       (uint16_t*)dya, (uint16_t*)nullptr, (uint16_t*)dz_out, n8, C8, C, msc, msh);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

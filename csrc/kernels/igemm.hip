@@ -44,6 +44,10 @@ struct IgemmParams {
   void* out;           // FWD/DGRAD: bf16 rows of Ncol; WGRAD: fp32 partial slab [splits][M][Ncol]
   float* stats;        // FWD: [m_tiles][2][Ncol] (Σy, Σy²) or nullptr
   const uint16_t* addend;   // DGRAD: optional bf16 tensor (same layout as out) added in the epilogue
+  // optional fused BatchNorm+ReLU on the activation operand as it is loaded (FWD: A = x,
+  // WGRAD: B = x): x' = max(x·in_scale[c] + in_shift[c], 0); padding taps stay exactly 0
+  const float* in_scale;
+  const float* in_shift;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -69,6 +73,23 @@ __device__ __forceinline__ int kout_off(int row, int ch) {
 }
 
 __device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// relu(x·s + t) on 8 packed bf16 channels (fp32 math, one rounding: same as bn_apply)
+__device__ __forceinline__ uint4 bnrelu8(uint4 v, const float (&s)[8], const float (&t)[8]) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = fmaxf(__uint_as_float(w[q] << 16) * s[2 * q] + t[2 * q], 0.f);
+    const float b = fmaxf(__uint_as_float(w[q] & 0xffff0000u) * s[2 * q + 1] + t[2 * q + 1], 0.f);
+    w[q] = pack_bf2(a, b);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 
 template <int MODE, int BM, int BN>
 struct Tile {
@@ -172,25 +193,49 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     wb_r = rs / g.S;
     wb_s = rs - wb_r * g.S;
   }
+  // WGRAD: fused BN+ReLU of the activation operand (channel chunk fixed per thread)
+  const bool wb_bn = (MODE == MODE_WGRAD) && p.in_scale != nullptr;
+  float wsc[8], wsh[8];
+  if (wb_bn) {
+    load8f(p.in_scale + wb_c, wsc);
+    load8f(p.in_shift + wb_c, wsh);
+  }
 
   uint4 ra[T::A_CH], rb[T::B_CH];
+  // fused BN+ReLU prologue: applied when the staged registers are written to LDS (after the
+  // MFMAs of the current tile), never right after the global load — that would put the
+  // load latency back on the critical path. Bit i of ld_mask = chunk i was loaded in-bounds
+  // (padding taps / tail rows stay exactly 0).
+  const bool bn_in = (MODE == MODE_FWD) && p.in_scale != nullptr;
+  float isc[8], ish[8];
+  unsigned ld_mask = 0;
 
   auto load_tile = [&](int k0) {
     if (MODE == MODE_FWD || MODE == MODE_DGRAD) {
       // A: gather 8 consecutive k (same tap, 8 channels) for each owned row
       const int k = k0 + kin_ch * 8;
       const bool kok = k < k_end;
+      if (bn_in) ld_mask = 0;
+      if (bn_in && kok) {
+        load8f(p.in_scale + kc, isc);
+        load8f(p.in_shift + kc, ish);
+      }
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (kok) {
           if (MODE == MODE_FWD) {
             if (is1x1) {
-              if (a_y[i] >= 0) v = ld16(p.a + a_base[i] + kc);
+              if (a_y[i] >= 0) {
+                v = ld16(p.a + a_base[i] + kc);
+                ld_mask |= 1u << i;
+              }
             } else {
               const int yy = a_y[i] + kr, xx = a_x[i] + ks;
-              if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W)
+              if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W) {
                 v = ld16(p.a + a_base[i] + (kr * g.W + ks) * g.C + kc);
+                ld_mask |= 1u << i;
+              }
             }
           } else {
             const int ty = a_y[i] - kr, tx = a_x[i] - ks;
@@ -225,6 +270,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         ra[i] = v;
       }
       // WGRAD B: im2col(x) rows (pixels) x BN (r,s,ci); the column chunk is fixed per thread
+      if (wb_bn) ld_mask = 0;
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
         const int e = tid + 256 * i;
@@ -234,14 +280,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         if (wb_ok && kk < k_end) {
           if (is1x1) {
             v = ld16(p.b + kk * g.C + wb_c);
+            ld_mask |= 1u << i;
           } else {
             const int n = (int)fdiv((unsigned)kk, p.div_pq);
             const int rem = kk - n * g.P * g.Q;
             const int pp = (int)fdiv((unsigned)rem, p.div_q);
             const int qq = rem - pp * g.Q;
             const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
-            if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W)
+            if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W) {
               v = ld16(p.b + ((n * g.H + yy) * g.W + xx) * g.C + wb_c);
+              ld_mask |= 1u << i;
+            }
           }
         }
         rb[i] = v;
@@ -252,6 +301,16 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   auto store_tile = [&](int buf) {
     unsigned char* sa = smem + buf * T::STAGE;
     unsigned char* sb = sa + T::A_BYTES;
+    if (bn_in) {
+#pragma unroll
+      for (int i = 0; i < T::A_CH; ++i)
+        if (ld_mask & (1u << i)) ra[i] = bnrelu8(ra[i], isc, ish);
+    }
+    if (wb_bn) {
+#pragma unroll
+      for (int i = 0; i < T::B_CH; ++i)
+        if (ld_mask & (1u << i)) rb[i] = bnrelu8(rb[i], wsc, wsh);
+    }
     if (MODE != MODE_WGRAD) {
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i)
@@ -525,8 +584,10 @@ int igemm_tile_m(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 256 : 64; }
 int igemm_tile_n(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 64 : cfg == 2 ? 256 : 64; }
 
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
-                           hipStream_t s) {
+                           hipStream_t s, const float* in_scale, const float* in_shift) {
   IgemmParams p{};
+  p.in_scale = in_scale;
+  p.in_shift = in_shift;
   p.g = g;
   p.a = (const uint16_t*)x;
   p.b = (const uint16_t*)w;
@@ -575,8 +636,11 @@ int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits) {
 }
 
 hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,
-                             int splits, int accumulate, hipStream_t s) {
+                             int splits, int accumulate, hipStream_t s, const float* in_scale,
+                             const float* in_shift) {
   IgemmParams p{};
+  p.in_scale = in_scale;
+  p.in_shift = in_shift;
   p.g = g;
   p.a = (const uint16_t*)dy;
   p.b = (const uint16_t*)x;

@@ -21,36 +21,45 @@ struct WSeg {
   long start;    // prefix sum of n
 };
 
+// blockIdx.y = conv (segment); blockIdx.x = 64(k) x 64(c) tile at one filter tap rs.
+// Reads of the fp32 master and writes of Wk are coalesced along c; the transposed Wt tile
+// goes through LDS so its writes are coalesced along k.
 __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ master, uint16_t* __restrict__ out,
-                                                    const WSeg* __restrict__ segs, int nseg, long total) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    int lo = 0, hi = nseg - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (segs[mid].start <= e) lo = mid; else hi = mid - 1;
+                                                    const WSeg* __restrict__ segs) {
+  __shared__ uint16_t tile[64][66];
+  const WSeg s = segs[blockIdx.y];
+  const int kt = (s.K + 63) / 64, ct = (s.Cp + 63) / 64;
+  int t = blockIdx.x;
+  if (t >= kt * ct * s.RS) return;
+  const int cti = t % ct; t /= ct;
+  const int rs = t % s.RS;
+  const int kti = t / s.RS;
+  const int k0 = kti * 64, c0 = cti * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int kk = ty; kk < 64; kk += 4) {
+    const int k = k0 + kk, c = c0 + tx;
+    if (k < s.K && c < s.Cp) {
+      const float v = c < s.C ? master[s.src + ((long)k * s.RS + rs) * s.C + c] : 0.f;
+      const uint16_t b = f2bf(v);
+      out[s.dst_k + ((long)k * s.RS + rs) * s.Cp + c] = b;
+      tile[kk][tx] = b;
     }
-    const WSeg s = segs[lo];
-    const long i = e - s.start;               // index into Wk [K][RS][Cp]
-    const int cp = (int)(i % s.Cp);
-    const long t = i / s.Cp;
-    const int rs = (int)(t % s.RS);
-    const int k = (int)(t / s.RS);
-    float v = 0.f;
-    if (cp < s.C) v = master[s.src + ((long)k * s.RS + rs) * s.C + cp];
-    const uint16_t b = f2bf(v);
-    out[s.dst_k + i] = b;
-    if (s.dst_t >= 0 && cp < s.C) out[s.dst_t + ((long)cp * s.RS + rs) * s.K + k] = b;
+  }
+  if (s.dst_t < 0) return;
+  __syncthreads();
+  for (int cc = ty; cc < 64; cc += 4) {
+    const int c = c0 + cc, k = k0 + tx;
+    if (c < s.C && k < s.K) out[s.dst_t + ((long)c * s.RS + rs) * s.K + k] = tile[tx][cc];
   }
 }
 
 }  // namespace
 
 hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s) {
-  long grid = (total + 255) / 256;
-  if (grid > 8192) grid = 8192;
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(wprep_kernel, dim3(grid), dim3(256), 0, s, master, (uint16_t*)out, (const WSeg*)segs, nseg,
-                     total);
+  // `total` = the largest conv's tile count (ceil(K/64)·ceil(Cp/64)·R·S), computed by the host
+  if (total < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wprep_kernel, dim3((unsigned)total, nseg), dim3(256), 0, s, master, (uint16_t*)out,
+                     (const WSeg*)segs);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

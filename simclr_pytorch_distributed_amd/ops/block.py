@@ -8,7 +8,12 @@ math: networks/resnet_big.py:7-67), which lets the executor
   split-K reduce, BN dγ/dβ from the coefficient kernel) — no AccumulateGrad adds;
 * fuse the residual-gradient sum into the last data-gradient GEMM epilogue
   (``dx = dgrad(conv1) + dgrad(shortcut) | + dz``) instead of a separate add pass;
-* run SyncBN as one fp64 all-reduce per BN per direction.
+* run SyncBN as one fp64 all-reduce per BN per direction;
+* never materialise the block-internal activations ``relu(bn1(y1))`` / ``relu(bn2(y2))``:
+  the consuming conv applies BN+ReLU in its operand-load prologue (forward and weight
+  gradient), and the BN backward recomputes the ReLU mask from ``y`` — saving one
+  write + two reads of every internal activation per step (``SDX_FUSE_PROLOGUE=0``
+  restores the materialised path).
 
 Parameters are passed to ``apply`` only to keep the autograd graph connected (their
 returned gradients are ``None``: the sinks already hold them); the bucket reducer is
@@ -16,12 +21,17 @@ notified through :mod:`ops.sinks`.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
 from . import _ext, sinks
+from .streams import SideWork
+
+
+FUSE_PROLOGUE = os.environ.get("SDX_FUSE_PROLOGUE", "1") != "0"
 
 
 def _world(group) -> int:
@@ -44,21 +54,33 @@ class _BN:
         return sc, sh, None, None
 
 
-def _conv(m, x, w, stride, pad, stats):
-    y, slab = m.conv_fwd(x, w, stride, pad, stats, -1)
+def _conv(m, x, w, stride, pad, stats, in_bn=None):
+    """conv (+BN stat slab); ``in_bn=(scale, shift)``: x is a pre-BN tensor and the
+    kernel feeds relu(x·scale + shift) to the GEMM."""
+    isc, ish = in_bn if in_bn is not None else (None, None)
+    y, slab = m.conv_fwd(x, w, stride, pad, stats, -1, isc, ish)
     return y, (m.bn_stats_reduce(slab) if stats else None)
 
 
+def _act(m, y, sc, sh):
+    """Block-internal BN+ReLU: returns (tensor the next conv reads, its prologue affine)."""
+    if FUSE_PROLOGUE:
+        return y, (sc, sh)
+    return m.bn_apply(y, sc, sh, None, None, None, 0, True), None
+
+
 def _bn_bwd(m, dout, out, y, mean, inv, bn, count, group, y_b=None, mean_b=None, inv_b=None, bn_b=None,
-            want_dz=False):
-    """BN(+second BN)+ReLU backward with dγ/dβ written into the parameter sinks."""
-    s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b)
+            want_dz=False, mask=None):
+    """BN(+second BN)+ReLU backward with dγ/dβ written into the parameter sinks.
+    ReLU mask from ``out``, or (``out`` None) from ``mask=(scale, shift)``: y·scale+shift > 0."""
+    msc, msh = mask if (out is None and mask is not None) else (None, None)
+    s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b, msc, msh)
     if group is not None:
         dist.all_reduce(s, group=group)
     if y_b is None:
         ca, _, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv,
                                           sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias))
-        dya, _, dz = m.bn_bwd_apply(dout, out, y, ca, None, None, want_dz)
+        dya, _, dz = m.bn_bwd_apply(dout, out, y, ca, None, None, want_dz, msc, msh)
         return dya, None, dz
     ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, bn_b.weight.detach(), mean_b,
                                        inv_b, sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias),
@@ -67,9 +89,16 @@ def _bn_bwd(m, dout, out, y, mean, inv, bn, count, group, y_b=None, mean_b=None,
     return dya, dyb, None
 
 
-def _wgrad(m, dy, x, cv, stride, pad):
+def _wgrad(m, dy, x, cv, stride, pad, in_bn=None):
+    """Weight gradient into the parameter sink, on the side stream (off the dgrad chain)."""
     R, S = cv.weight.shape[2], cv.weight.shape[3]
-    m.conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sinks.target(cv.weight), True)
+    sink = sinks.target(cv.weight)
+    if in_bn is None:
+        with SideWork(dy, x):
+            m.conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, True)
+    else:
+        with SideWork(dy, x, *in_bn):
+            m.conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, True, in_bn[0], in_bn[1])
 
 
 class _Bottleneck(torch.autograd.Function):
@@ -81,12 +110,12 @@ class _Bottleneck(torch.autograd.Function):
         y1, s1 = _conv(m, x, wc.fwd(blk.conv1), 1, 0, training)
         cnt1 = (y1.numel() // y1.shape[-1]) * _world(group)
         sc1, sh1, mu1, iv1 = _BN.forward(m, s1, blk.bn1, cnt1, training, group)
-        a1 = m.bn_apply(y1, sc1, sh1, None, None, None, 0, True)
-        y2, s2 = _conv(m, a1, wc.fwd(blk.conv2), st, 1, training)
+        a1, f1 = _act(m, y1, sc1, sh1)
+        y2, s2 = _conv(m, a1, wc.fwd(blk.conv2), st, 1, training, f1)
         cnt2 = (y2.numel() // y2.shape[-1]) * _world(group)
         sc2, sh2, mu2, iv2 = _BN.forward(m, s2, blk.bn2, cnt2, training, group)
-        a2 = m.bn_apply(y2, sc2, sh2, None, None, None, 0, True)
-        y3, s3 = _conv(m, a2, wc.fwd(blk.conv3), 1, 0, training)
+        a2, f2 = _act(m, y2, sc2, sh2)
+        y3, s3 = _conv(m, a2, wc.fwd(blk.conv3), 1, 0, training, f2)
         sc3, sh3, mu3, iv3 = _BN.forward(m, s3, blk.bn3, cnt2, training, group)
         ys = mus = ivs = None
         if proj:
@@ -96,7 +125,9 @@ class _Bottleneck(torch.autograd.Function):
         else:
             out = m.bn_apply(y3, sc3, sh3, x, None, None, 2, True)
         if training:
-            ctx.save_for_backward(x, y1, a1, y2, a2, y3, ys, out, mu1, iv1, mu2, iv2, mu3, iv3, mus, ivs)
+            fused = f1 is not None
+            ctx.save_for_backward(x, y1, None if fused else a1, y2, None if fused else a2, y3, ys, out, mu1, iv1,
+                                  mu2, iv2, mu3, iv3, mus, ivs, sc1, sh1, sc2, sh2)
             ctx.blk, ctx.wc, ctx.group, ctx.params = blk, wc, group, params
             ctx.cnt = (cnt1, cnt2)
         return out
@@ -104,7 +135,9 @@ class _Bottleneck(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         m = _ext.require()
-        x, y1, a1, y2, a2, y3, ys, out, mu1, iv1, mu2, iv2, mu3, iv3, mus, ivs = ctx.saved_tensors
+        x, y1, a1, y2, a2, y3, ys, out, mu1, iv1, mu2, iv2, mu3, iv3, mus, ivs, sc1, sh1, sc2, sh2 = ctx.saved_tensors
+        f1 = (sc1, sh1) if a1 is None else None
+        f2 = (sc2, sh2) if a2 is None else None
         blk, wc, group = ctx.blk, ctx.wc, ctx.group
         cnt1, cnt2 = ctx.cnt
         st = blk.stride
@@ -116,12 +149,12 @@ class _Bottleneck(torch.autograd.Function):
             dz = None
         else:
             dy3, _, dz = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group, want_dz=True)
-        _wgrad(m, dy3, a2, blk.conv3, 1, 0)
+        _wgrad(m, dy3, y2 if f2 else a2, blk.conv3, 1, 0, f2)
         da2 = m.conv_dgrad(dy3, wc.dgrad(blk.conv3), y2.shape[1], y2.shape[2], 1, 0)
-        dy2, _, _ = _bn_bwd(m, da2, a2, y2, mu2, iv2, blk.bn2, cnt2, group)
-        _wgrad(m, dy2, a1, blk.conv2, st, 1)
+        dy2, _, _ = _bn_bwd(m, da2, a2, y2, mu2, iv2, blk.bn2, cnt2, group, mask=f2)
+        _wgrad(m, dy2, y1 if f1 else a1, blk.conv2, st, 1, f1)
         da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), H, W, st, 1)
-        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt1, group)
+        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt1, group, mask=f1)
         _wgrad(m, dy1, x, blk.conv1, 1, 0)
         if proj:
             _wgrad(m, dys, x, blk.shortcut[0], st, 0)
@@ -142,8 +175,8 @@ class _Basic(torch.autograd.Function):
         y1, s1 = _conv(m, x, wc.fwd(blk.conv1), st, 1, training)
         cnt = (y1.numel() // y1.shape[-1]) * _world(group)
         sc1, sh1, mu1, iv1 = _BN.forward(m, s1, blk.bn1, cnt, training, group)
-        a1 = m.bn_apply(y1, sc1, sh1, None, None, None, 0, True)
-        y2, s2 = _conv(m, a1, wc.fwd(blk.conv2), 1, 1, training)
+        a1, f1 = _act(m, y1, sc1, sh1)
+        y2, s2 = _conv(m, a1, wc.fwd(blk.conv2), 1, 1, training, f1)
         sc2, sh2, mu2, iv2 = _BN.forward(m, s2, blk.bn2, cnt, training, group)
         ys = mus = ivs = None
         if proj:
@@ -153,14 +186,16 @@ class _Basic(torch.autograd.Function):
         else:
             out = m.bn_apply(y2, sc2, sh2, x, None, None, 2, True)
         if training:
-            ctx.save_for_backward(x, y1, a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs)
+            ctx.save_for_backward(x, y1, None if f1 is not None else a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs,
+                                  sc1, sh1)
             ctx.blk, ctx.wc, ctx.group, ctx.params, ctx.cnt = blk, wc, group, params, cnt
         return out
 
     @staticmethod
     def backward(ctx, dout):
         m = _ext.require()
-        x, y1, a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs = ctx.saved_tensors
+        x, y1, a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs, sc1, sh1 = ctx.saved_tensors
+        f1 = (sc1, sh1) if a1 is None else None
         blk, wc, group, cnt = ctx.blk, ctx.wc, ctx.group, ctx.cnt
         st = blk.stride
         H, W = x.shape[1], x.shape[2]
@@ -171,9 +206,9 @@ class _Basic(torch.autograd.Function):
             dz = None
         else:
             dy2, _, dz = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group, want_dz=True)
-        _wgrad(m, dy2, a1, blk.conv2, 1, 1)
+        _wgrad(m, dy2, y1 if f1 else a1, blk.conv2, 1, 1, f1)
         da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), y1.shape[1], y1.shape[2], 1, 1)
-        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt, group)
+        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt, group, mask=f1)
         _wgrad(m, dy1, x, blk.conv1, st, 1)
         if proj:
             _wgrad(m, dys, x, blk.shortcut[0], st, 0)
@@ -213,9 +248,10 @@ class _Stem(torch.autograd.Function):
         dy, _, _ = _bn_bwd(m, da, a, y, mu, iv, ctx.enc.bn1, ctx.cnt, ctx.group)
         w = ctx.enc.conv1.weight
         K, C, R, S = w.shape
-        dwk = m.conv_wgrad(dy, x, R, S, st, pad, 0, -1)          # [K][R][S][Cp] fp32
         g = sinks.target(w)
-        g.add_(dwk[..., :C].permute(0, 3, 1, 2))
+        with SideWork(dy, x):
+            dwk = m.conv_wgrad(dy, x, R, S, st, pad, 0, -1)      # [K][R][S][Cp] fp32
+            g.add_(dwk[..., :C].permute(0, 3, 1, 2))
         sinks.notify(ctx.params)
         return (None, None, None, None, None) + (None,) * len(ctx.params)
 

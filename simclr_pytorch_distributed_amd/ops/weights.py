@@ -50,6 +50,8 @@ class ConvWeightCache:
                         ok = False
                     rows.append([src, e["off_k"], e["off_t"], K | ((R * S) << 32), C | (Cp << 32), n_k, start])
                     start += n_k
+                    tiles = ((K + 63) // 64) * ((Cp + 63) // 64) * R * S
+                    self.max_tiles = max(getattr(self, "max_tiles", 0), tiles)
         self.total = start
         self.buf = torch.empty(off, dtype=torch.bfloat16, device=dev)
         self.native = ok and dev.type == "cuda" and _ext.available()
@@ -59,7 +61,7 @@ class ConvWeightCache:
     def refresh(self):
         """Re-derive all bf16 copies from the current fp32 master weights (one launch)."""
         if self.native:
-            _ext.require().wprep(self.master, self.buf, self.segs, self.total)
+            _ext.require().wprep(self.master, self.buf, self.segs, self.max_tiles)
         else:
             for cv in self.convs:
                 e = self.entries[id(cv)]

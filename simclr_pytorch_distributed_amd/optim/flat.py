@@ -93,6 +93,12 @@ class _FlatOptimizer:
         self.grad_scale = 1.0
         self.steps = 0
 
+    def _join(self):
+        """Weight gradients may still be in flight on the wgrad side stream."""
+        if self.flat.grad.is_cuda:
+            from ..ops import streams
+            streams.join(self.flat.grad.device)
+
     def _sync_lr(self):
         if self.lr_t.is_cuda and torch.cuda.is_current_stream_capturing():
             return   # the host-side lr write must stay outside a captured graph
@@ -136,6 +142,7 @@ class FusedSGD(_FlatOptimizer):
     @torch.no_grad()
     def step(self):
         self._sync_lr()
+        self._join()
         f = self.flat
         if self.native:
             _ext.require().sgd_step(f.flat, f.grad, self.buf, self.lr_t, self.momentum, self.weight_decay,
@@ -167,6 +174,7 @@ class FusedLARS(_FlatOptimizer):
     @torch.no_grad()
     def step(self):
         self._sync_lr()
+        self._join()
         f = self.flat
         if self.native:
             _ext.require().lars_step(f.flat, f.grad, self.buf, self.seg_off, self.adapt, self.lr_t, self.momentum,

@@ -94,6 +94,10 @@ class GradBucketReducer:
             ev = torch.cuda.current_stream().record_event()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                # fused blocks compute weight gradients on the wgrad side stream
+                from ..ops import streams
+                if streams.ENABLED:
+                    self.comm_stream.wait_stream(streams.side(view.device))
                 b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
         else:
             b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
@@ -102,6 +106,9 @@ class GradBucketReducer:
         """Wait for all bucket reductions (launching any bucket whose params got no grad)."""
         if not self.enabled:
             return
+        if self.is_cuda:
+            from ..ops import streams
+            streams.join(self.flat.grad.device)
         for b in self.buckets:
             if b["work"] is None:
                 self._launch(b)

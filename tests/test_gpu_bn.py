@@ -79,3 +79,26 @@ def test_bn_eval_affine(gpu):
     out = m.bn_apply(y, sc, sh, None, None, None, 0, False)
     ref = F.batch_norm(y.float().permute(0, 3, 1, 2), rm, rv, g, b, training=False, eps=1e-5)
     assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_bn_bwd_mask_from_input(gpu):
+    """bn_bwd_reduce/apply with the ReLU mask recomputed from y (msc/msh) == with the
+    stored activation."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(1)
+    N, H, W, C = 8, 8, 8, 64
+    y = (torch.randn(N, H, W, C, device=gpu) + 0.2).bfloat16()
+    g1, b1 = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    flat = y.reshape(-1, C).float()
+    sums = torch.stack([flat.sum(0), (flat * flat).sum(0)]).double().contiguous()
+    sc, sh, mean, inv = m.bn_finalize(sums, float(N * H * W), g1, b1, 1e-5, 0.1, False, None, None)
+    a = m.bn_apply(y, sc, sh, None, None, None, 0, True)
+    dout = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    s_ref = m.bn_bwd_reduce(dout, a, y, mean)
+    s = m.bn_bwd_reduce(dout, None, y, mean, msc=sc, msh=sh)
+    assert torch.allclose(s, s_ref, rtol=1e-4, atol=1e-3)
+    ca = m.bn_bwd_coef(s_ref, float(N * H * W), g1, mean, inv)[0]
+    d_ref = m.bn_bwd_apply(dout, a, y, ca)[0]
+    d = m.bn_bwd_apply(dout, None, y, ca, msc=sc, msh=sh)[0]
+    assert _rel(d, d_ref) < 1e-2

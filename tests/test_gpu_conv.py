@@ -119,3 +119,29 @@ def test_conv_wgrad_into_sink_accumulate(gpu):
     assert _rel(sink - 1, dw_ref) < 5e-3
     m.conv_wgrad(dyh, xh, R, R, st, pad, 1, -1, sink, False)
     assert _rel(sink, dw_ref) < 5e-3
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[3] % 8 == 0 and s[3] > 8])
+@pytest.mark.parametrize("cfg", [0, 3])
+def test_conv_bn_relu_prologue(gpu, shape, cfg):
+    """conv_fwd / conv_wgrad with in_scale/in_shift == the same conv on the materialised
+    relu(y·scale + shift) (bf16), incl. zero padding taps staying zero."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, W, C, K, R, st, pad = shape
+    y, w = _mk(N, H, W, C, K, R, seed=3)
+    yh = y.permute(0, 2, 3, 1).contiguous()
+    wh = w.permute(0, 2, 3, 1).contiguous()
+    g = torch.Generator(device="cpu").manual_seed(4)
+    sc = (torch.rand(C, generator=g) + 0.5).cuda()
+    sh = (torch.randn(C, generator=g) * 0.5).cuda()
+    a = torch.relu(yh.float() * sc + sh).bfloat16()
+    ref, slab_ref = m.conv_fwd(a, wh, st, pad, True, cfg)
+    out, slab = m.conv_fwd(yh, wh, st, pad, True, cfg, sc, sh)
+    assert _rel(out, ref) < 1e-2
+    s_ref, s = m.bn_stats_reduce(slab_ref), m.bn_stats_reduce(slab)
+    assert torch.allclose(s, s_ref, rtol=1e-3, atol=1e-1)
+    dy = torch.randn(out.shape, generator=g).cuda().bfloat16()
+    dw_ref = m.conv_wgrad(dy, a, R, R, st, pad, 0, cfg)
+    dw = m.conv_wgrad(dy, yh, R, R, st, pad, 0, cfg, None, False, sc, sh)
+    assert _rel(dw, dw_ref) < 1e-2

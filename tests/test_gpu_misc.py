@@ -83,8 +83,12 @@ def test_native_blocks_teacher_forced(gpu):
 
 
 @pytest.mark.parametrize("name", ["resnet18", "resnet50"])
-def test_fused_blocks_match_unfused(gpu, name):
-    """Fused block autograd (weight cache, grad sinks, fused residual-grad) == per-op path."""
+@pytest.mark.parametrize("prologue", [True, False])
+def test_fused_blocks_match_unfused(gpu, name, prologue, monkeypatch):
+    """Fused block autograd (weight cache, grad sinks, fused residual-grad, with/without the
+    BN+ReLU conv prologue) == per-op path."""
+    from simclr_pytorch_distributed_amd.ops import block
+    monkeypatch.setattr(block, "FUSE_PROLOGUE", prologue)
     from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
     from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams
@@ -100,6 +104,7 @@ def test_fused_blocks_match_unfused(gpu, name):
     for r, f in ((ra, fa), (rb, fb)):
         f.zero_grad()
         (r.forward(x) * w).sum().backward()
+    torch.cuda.synchronize()   # wgrads run on the side stream
     assert torch.equal(a.encoder.layer1[0].bn1.running_mean, b.encoder.layer1[0].bn1.running_mean)
     assert torch.equal(a.encoder.bn1.num_batches_tracked, b.encoder.bn1.num_batches_tracked)
     ga, gb = fa.grad, fb.grad
