@@ -3,6 +3,9 @@
 #include "ops_decl.h"
 #include "launchers.h"
 
+#include <map>
+#include <mutex>
+
 namespace sdx_bind {
 namespace {
 
@@ -183,16 +186,77 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   return dw;
 }
 
-torch::Tensor bn_stats_reduce(torch::Tensor slab) {
-  TORCH_CHECK(slab.is_cuda() && slab.scalar_type() == at::kFloat && slab.dim() == 3 && slab.size(1) == 2 &&
+// Ticket counters of the single-launch column reduction: zeroed once per device, reset by
+// each launch's last block; consecutive launches rotate through slots so launches on
+// different streams never share a counter.
+unsigned* reduce_counters(const torch::Device& dev) {
+  constexpr int kSlots = 256, kPerSlot = 64;   // 64 column groups = 4096 channels
+  static std::mutex mu;
+  static std::map<int, std::pair<torch::Tensor, int>> pool;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = pool[dev.index()];
+  if (!e.first.defined())
+    e.first = torch::zeros({kSlots * kPerSlot}, torch::TensorOptions().dtype(at::kInt).device(dev));
+  const int slot = e.second;
+  e.second = (slot + 1) % kSlots;
+  return reinterpret_cast<unsigned*>(e.first.data_ptr<int>()) + slot * kPerSlot;
+}
+
+void check_slab(const torch::Tensor& slab, int64_t nsets) {
+  TORCH_CHECK(slab.is_cuda() && slab.scalar_type() == at::kFloat && slab.dim() == 3 && slab.size(1) == nsets &&
                   slab.is_contiguous(),
-              "slab must be [rows, 2, C] float32");
+              "slab must be [rows, ", nsets, ", C] float32");
+  TORCH_CHECK(slab.size(2) <= 4096, "C <= 4096");
+}
+
+torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t nsets, int64_t C) {
+  return torch::empty({col_reduce_gy((int)rows) * nsets * C}, like.options().dtype(at::kDouble));
+}
+
+torch::Tensor bn_stats_reduce(torch::Tensor slab) {
+  check_slab(slab, 2);
   c10::DeviceGuard dg(slab.device());
-  const int64_t C = slab.size(2);
+  const int64_t rows = slab.size(0), C = slab.size(2);
   auto out = torch::empty({2, C}, slab.options().dtype(at::kDouble));
-  check_hip(launch_bn_stats_reduce(slab.data_ptr<float>(), slab.size(0), C, out.data_ptr<double>(), cur_stream()),
+  auto scratch = reduce_scratch(slab, rows, 2, C);
+  check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, 2, C, scratch.data_ptr<double>(),
+                              reduce_counters(slab.device()), out.data_ptr<double>(), 0, nullptr, nullptr,
+                              cur_stream()),
             "bn_stats_reduce");
   return out;
+}
+
+struct FinalizeOut {
+  torch::Tensor scale, shift, mean, invstd;
+};
+
+BnFinalizeArgs finalize_args(const torch::Tensor& like, int64_t C, double count, const OptT& gamma, const OptT& beta,
+                             double eps, double momentum, bool update, const OptT& running_mean,
+                             const OptT& running_var, FinalizeOut& o) {
+  BnFinalizeArgs a{};
+  a.count = count;
+  a.gamma = opt_ptr(gamma, C, "gamma");
+  a.beta = opt_ptr(beta, C, "beta");
+  a.eps = (float)eps;
+  a.momentum = (float)momentum;
+  a.update_running = update ? 1 : 0;
+  if (update) {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "running stats required for update");
+    check_vec(*running_mean, C, "running_mean");
+    check_vec(*running_var, C, "running_var");
+    a.running_mean = running_mean->data_ptr<float>();
+    a.running_var = running_var->data_ptr<float>();
+  }
+  auto fo = like.options().dtype(at::kFloat);
+  o.scale = torch::empty({C}, fo);
+  o.shift = torch::empty({C}, fo);
+  o.mean = torch::empty({C}, fo);
+  o.invstd = torch::empty({C}, fo);
+  a.scale = o.scale.data_ptr<float>();
+  a.shift = o.shift.data_ptr<float>();
+  a.mean = o.mean.data_ptr<float>();
+  a.invstd = o.invstd.data_ptr<float>();
+  return a;
 }
 
 std::vector<torch::Tensor> bn_finalize(torch::Tensor sums, double count, OptT gamma, OptT beta, double eps,
@@ -202,25 +266,28 @@ std::vector<torch::Tensor> bn_finalize(torch::Tensor sums, double count, OptT ga
               "sums must be [2, C] float64");
   const int64_t C = sums.size(1);
   c10::DeviceGuard dg(sums.device());
-  const float* gp = opt_ptr(gamma, C, "gamma");
-  const float* bp = opt_ptr(beta, C, "beta");
-  float* rm = nullptr;
-  float* rv = nullptr;
-  if (update) {
-    TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "running stats required for update");
-    check_vec(*running_mean, C, "running_mean");
-    check_vec(*running_var, C, "running_var");
-    rm = running_mean->data_ptr<float>();
-    rv = running_var->data_ptr<float>();
-  }
-  auto fo = sums.options().dtype(at::kFloat);
-  auto scale = torch::empty({C}, fo), shift = torch::empty({C}, fo);
-  auto mean = torch::empty({C}, fo), invstd = torch::empty({C}, fo);
-  check_hip(launch_bn_finalize(sums.data_ptr<double>(), C, count, gp, bp, (float)eps, (float)momentum, update ? 1 : 0,
-                               rm, rv, scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
-                               invstd.data_ptr<float>(), cur_stream()),
-            "bn_finalize");
-  return {scale, shift, mean, invstd};
+  FinalizeOut o;
+  const BnFinalizeArgs a =
+      finalize_args(sums, C, count, gamma, beta, eps, momentum, update, running_mean, running_var, o);
+  check_hip(launch_bn_finalize(sums.data_ptr<double>(), C, a, cur_stream()), "bn_finalize");
+  return {o.scale, o.shift, o.mean, o.invstd};
+}
+
+// conv stat slab -> (scale, shift, mean, invstd) in ONE launch (no cross-rank reduction)
+std::vector<torch::Tensor> bn_stats_finalize(torch::Tensor slab, double count, OptT gamma, OptT beta, double eps,
+                                             double momentum, bool update, OptT running_mean, OptT running_var) {
+  check_slab(slab, 2);
+  c10::DeviceGuard dg(slab.device());
+  const int64_t rows = slab.size(0), C = slab.size(2);
+  FinalizeOut o;
+  const BnFinalizeArgs a =
+      finalize_args(slab, C, count, gamma, beta, eps, momentum, update, running_mean, running_var, o);
+  auto sums = torch::empty({2, C}, slab.options().dtype(at::kDouble));
+  auto scratch = reduce_scratch(slab, rows, 2, C);
+  check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, 2, C, scratch.data_ptr<double>(),
+                              reduce_counters(slab.device()), sums.data_ptr<double>(), 1, &a, nullptr, cur_stream()),
+            "bn_stats_finalize");
+  return {o.scale, o.shift, o.mean, o.invstd};
 }
 
 std::vector<torch::Tensor> bn_eval_affine(OptT gamma, OptT beta, torch::Tensor rm, torch::Tensor rv, double eps) {
@@ -268,46 +335,115 @@ void check_bwd_C(int64_t C) {
   TORCH_CHECK(C <= 2048 && (C & (C - 1)) == 0 && C >= 8, "bn backward supports power-of-two C in [8, 2048]");
 }
 
-// ReLU mask: from the stored activation `outv`, or (outv None, msc/msh given) recomputed as
-// ya·msc + msh > 0 for an activation that was never materialised
-torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
-                            OptT msc, OptT msh) {
+struct BwdIn {
+  const void* op = nullptr;
+  const void* ybp = nullptr;
+  const float* mbp = nullptr;
+  const float* mk_s = nullptr;
+  const float* mk_t = nullptr;
+  int64_t C = 0;
+};
+
+BwdIn bwd_inputs(const torch::Tensor& dout, const OptT& outv, const torch::Tensor& ya, const torch::Tensor& ma,
+                 const OptT& yb, const OptT& mb, const OptT& msc, const OptT& msh) {
+  BwdIn in;
   check_bf16_nhwc(dout, "dout");
   check_bf16_nhwc(ya, "ya");
-  const int64_t C = dout.size(3);
-  check_bwd_C(C);
+  in.C = dout.size(3);
+  check_bwd_C(in.C);
   TORCH_CHECK(ya.sizes() == dout.sizes(), "ya shape");
-  check_vec(ma, C, "mean_a");
-  const void* op = nullptr;
+  check_vec(ma, in.C, "mean_a");
   if (outv.has_value()) {
     check_bf16_nhwc(*outv, "out");
     TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
-    op = outv->data_ptr();
+    in.op = outv->data_ptr();
   }
-  const void* ybp = nullptr;
-  const float* mbp = nullptr;
   if (yb.has_value()) {
     check_bf16_nhwc(*yb, "yb");
     TORCH_CHECK(yb->sizes() == dout.sizes(), "yb shape");
     TORCH_CHECK(mb.has_value(), "mean_b required");
-    check_vec(*mb, C, "mean_b");
-    ybp = yb->data_ptr();
-    mbp = mb->data_ptr<float>();
+    check_vec(*mb, in.C, "mean_b");
+    in.ybp = yb->data_ptr();
+    in.mbp = mb->data_ptr<float>();
   }
+  in_bn_ptrs(msc, msh, in.C, &in.mk_s, &in.mk_t);
+  return in;
+}
+
+// ReLU mask: from the stored activation `outv`, or (outv None, msc/msh given) recomputed as
+// ya·msc + msh > 0 for an activation that was never materialised
+torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
+                            OptT msc, OptT msh) {
+  const BwdIn in = bwd_inputs(dout, outv, ya, ma, yb, mb, msc, msh);
   c10::DeviceGuard dg(dout.device());
-  const float *mk_s, *mk_t;
-  in_bn_ptrs(msc, msh, C, &mk_s, &mk_t);
-  const int nsets = ybp ? 3 : 2;
+  const int64_t C = in.C;
+  const int nsets = in.ybp ? 3 : 2;
+  const int g = bn_bwd_reduce_blocks(dout.numel(), C);
   auto sums = torch::empty({nsets, C}, dout.options().dtype(at::kDouble));
-  auto partial = torch::empty({bn_bwd_reduce_blocks(dout.numel(), C), nsets, C}, dout.options().dtype(at::kFloat));
-  check_hip(launch_bn_bwd_reduce(dout.data_ptr(), op, ya.data_ptr(), ma.data_ptr<float>(), ybp, mbp, dout.numel(), C,
-                                 partial.data_ptr<float>(), sums.data_ptr<double>(), cur_stream(), mk_s, mk_t),
+  auto partial = torch::empty({g, nsets, C}, dout.options().dtype(at::kFloat));
+  auto scratch = reduce_scratch(dout, g, nsets, C);
+  check_hip(launch_bn_bwd_reduce(dout.data_ptr(), in.op, ya.data_ptr(), ma.data_ptr<float>(), in.ybp, in.mbp,
+                                 dout.numel(), C, partial.data_ptr<float>(), scratch.data_ptr<double>(),
+                                 reduce_counters(dout.device()), sums.data_ptr<double>(), 0, nullptr, cur_stream(),
+                                 in.mk_s, in.mk_t),
             "bn_bwd_reduce");
   return sums;
 }
 
+struct CoefOut {
+  torch::Tensor coef_a, coef_b, dga, dba, dgb, dbb;
+};
+
 // dγ/dβ go to freshly allocated tensors, or are ADDED into caller-provided gradient
 // sinks (sink_ga, sink_ba, sink_gb, sink_bb: the parameters' .grad views).
+BnCoefArgs coef_args(const torch::Tensor& like, int64_t C, int nsets, double count, const OptT& g_a,
+                     const torch::Tensor& mean_a, const torch::Tensor& inv_a, const OptT& g_b, const OptT& mean_b,
+                     const OptT& inv_b, const OptT& sink_ga, const OptT& sink_ba, const OptT& sink_gb,
+                     const OptT& sink_bb, CoefOut& o) {
+  TORCH_CHECK(nsets == 1 || nsets == 2, "1 or 2 BN sets");
+  check_vec(mean_a, C, "mean_a");
+  check_vec(inv_a, C, "inv_a");
+  auto fo = like.options().dtype(at::kFloat);
+  const bool sinks = sink_ga.has_value();
+  TORCH_CHECK(!sinks || (sink_ba.has_value() && (nsets == 1 || (sink_gb.has_value() && sink_bb.has_value()))),
+              "all gradient sinks must be given together");
+  BnCoefArgs a{};
+  a.count = count;
+  a.accumulate = sinks ? 1 : 0;
+  o.coef_a = torch::empty({3, C}, fo);
+  o.dga = sinks ? *sink_ga : torch::empty({C}, fo);
+  o.dba = sinks ? *sink_ba : torch::empty({C}, fo);
+  if (sinks) {
+    check_vec(o.dga, C, "sink_ga");
+    check_vec(o.dba, C, "sink_ba");
+  }
+  a.g_a = opt_ptr(g_a, C, "g_a");
+  a.mean_a = mean_a.data_ptr<float>();
+  a.inv_a = inv_a.data_ptr<float>();
+  a.coef_a = o.coef_a.data_ptr<float>();
+  a.dgamma_a = o.dga.data_ptr<float>();
+  a.dbeta_a = o.dba.data_ptr<float>();
+  if (nsets == 2) {
+    o.coef_b = torch::empty({3, C}, fo);
+    o.dgb = sinks ? *sink_gb : torch::empty({C}, fo);
+    o.dbb = sinks ? *sink_bb : torch::empty({C}, fo);
+    if (sinks) {
+      check_vec(o.dgb, C, "sink_gb");
+      check_vec(o.dbb, C, "sink_bb");
+    }
+    a.g_b = opt_ptr(g_b, C, "g_b");
+    a.mean_b = opt_ptr(mean_b, C, "mean_b");
+    a.inv_b = opt_ptr(inv_b, C, "inv_b");
+    TORCH_CHECK(a.mean_b && a.inv_b, "mean_b/inv_b required");
+    a.coef_b = o.coef_b.data_ptr<float>();
+    a.dgamma_b = o.dgb.data_ptr<float>();
+    a.dbeta_b = o.dbb.data_ptr<float>();
+  } else {
+    o.coef_b = o.dgb = o.dbb = torch::empty({0}, fo);
+  }
+  return a;
+}
+
 std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_a, torch::Tensor mean_a,
                                        torch::Tensor inv_a, OptT g_b, OptT mean_b, OptT inv_b, OptT sink_ga,
                                        OptT sink_ba, OptT sink_gb, OptT sink_bb) {
@@ -315,45 +451,37 @@ std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_
               "sums must be [nsets+1, C] float64");
   const int64_t C = sums.size(1);
   const int nsets = (int)sums.size(0) - 1;
-  TORCH_CHECK(nsets == 1 || nsets == 2, "1 or 2 BN sets");
-  check_vec(mean_a, C, "mean_a");
-  check_vec(inv_a, C, "inv_a");
   c10::DeviceGuard dg(sums.device());
-  auto fo = sums.options().dtype(at::kFloat);
-  const bool sinks = sink_ga.has_value();
-  TORCH_CHECK(!sinks || (sink_ba.has_value() && (nsets == 1 || (sink_gb.has_value() && sink_bb.has_value()))),
-              "all gradient sinks must be given together");
-  auto coef_a = torch::empty({3, C}, fo);
-  torch::Tensor dga = sinks ? *sink_ga : torch::empty({C}, fo), dba = sinks ? *sink_ba : torch::empty({C}, fo);
-  if (sinks) {
-    check_vec(dga, C, "sink_ga");
-    check_vec(dba, C, "sink_ba");
-  }
-  torch::Tensor coef_b, dgb, dbb;
-  const float *gbp = nullptr, *mbp = nullptr, *ibp = nullptr;
-  if (nsets == 2) {
-    coef_b = torch::empty({3, C}, fo);
-    dgb = sinks ? *sink_gb : torch::empty({C}, fo);
-    dbb = sinks ? *sink_bb : torch::empty({C}, fo);
-    if (sinks) {
-      check_vec(dgb, C, "sink_gb");
-      check_vec(dbb, C, "sink_bb");
-    }
-    gbp = opt_ptr(g_b, C, "g_b");
-    mbp = opt_ptr(mean_b, C, "mean_b");
-    ibp = opt_ptr(inv_b, C, "inv_b");
-    TORCH_CHECK(mbp && ibp, "mean_b/inv_b required");
-  } else {
-    coef_b = dgb = dbb = torch::empty({0}, fo);
-  }
-  check_hip(launch_bn_bwd_coef(sums.data_ptr<double>(), nsets, C, count, opt_ptr(g_a, C, "g_a"),
-                               mean_a.data_ptr<float>(), inv_a.data_ptr<float>(), gbp, mbp, ibp,
-                               coef_a.data_ptr<float>(), nsets == 2 ? coef_b.data_ptr<float>() : nullptr,
-                               dga.data_ptr<float>(), dba.data_ptr<float>(),
-                               nsets == 2 ? dgb.data_ptr<float>() : nullptr,
-                               nsets == 2 ? dbb.data_ptr<float>() : nullptr, sinks ? 1 : 0, cur_stream()),
-            "bn_bwd_coef");
-  return {coef_a, coef_b, dga, dba, dgb, dbb};
+  CoefOut o;
+  const BnCoefArgs a = coef_args(sums, C, nsets, count, g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga, sink_ba,
+                                 sink_gb, sink_bb, o);
+  check_hip(launch_bn_bwd_coef(sums.data_ptr<double>(), nsets, C, a, cur_stream()), "bn_bwd_coef");
+  return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
+}
+
+// bn_bwd_reduce + bn_bwd_coef in one elementwise launch + one reduction launch (no
+// cross-rank all-reduce of the sums in between)
+std::vector<torch::Tensor> bn_bwd_reduce_coef(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma,
+                                              OptT yb, OptT mb, OptT msc, OptT msh, double count, OptT g_a,
+                                              torch::Tensor inv_a, OptT g_b, OptT inv_b, OptT sink_ga, OptT sink_ba,
+                                              OptT sink_gb, OptT sink_bb) {
+  const BwdIn in = bwd_inputs(dout, outv, ya, ma, yb, mb, msc, msh);
+  c10::DeviceGuard dg(dout.device());
+  const int64_t C = in.C;
+  const int nsum = in.ybp ? 3 : 2;
+  CoefOut o;
+  const BnCoefArgs a = coef_args(dout, C, nsum - 1, count, g_a, ma, inv_a, g_b, mb, inv_b, sink_ga, sink_ba, sink_gb,
+                                 sink_bb, o);
+  const int g = bn_bwd_reduce_blocks(dout.numel(), C);
+  auto sums = torch::empty({nsum, C}, dout.options().dtype(at::kDouble));
+  auto partial = torch::empty({g, nsum, C}, dout.options().dtype(at::kFloat));
+  auto scratch = reduce_scratch(dout, g, nsum, C);
+  check_hip(launch_bn_bwd_reduce(dout.data_ptr(), in.op, ya.data_ptr(), ma.data_ptr<float>(), in.ybp, in.mbp,
+                                 dout.numel(), C, partial.data_ptr<float>(), scratch.data_ptr<double>(),
+                                 reduce_counters(dout.device()), sums.data_ptr<double>(), 2, &a, cur_stream(),
+                                 in.mk_s, in.mk_t),
+            "bn_bwd_reduce_coef");
+  return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
 }
 
 std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ca, OptT yb,
@@ -412,6 +540,7 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("in_shift") = pybind11::none());
   m.def("bn_stats_reduce", &bn_stats_reduce);
   m.def("bn_finalize", &bn_finalize);
+  m.def("bn_stats_finalize", &bn_stats_finalize, "conv stat slab -> BN affine in one launch");
   m.def("bn_eval_affine", &bn_eval_affine);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
@@ -422,6 +551,14 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("mean_b") = pybind11::none(), pybind11::arg("inv_b") = pybind11::none(),
         pybind11::arg("sink_ga") = pybind11::none(), pybind11::arg("sink_ba") = pybind11::none(),
         pybind11::arg("sink_gb") = pybind11::none(), pybind11::arg("sink_bb") = pybind11::none());
+  m.def("bn_bwd_reduce_coef", &bn_bwd_reduce_coef, pybind11::arg("dout"), pybind11::arg("outv"),
+        pybind11::arg("ya"), pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(),
+        pybind11::arg("mb") = pybind11::none(), pybind11::arg("msc") = pybind11::none(),
+        pybind11::arg("msh") = pybind11::none(), pybind11::arg("count") = 1.0, pybind11::arg("g_a") = pybind11::none(),
+        pybind11::arg("inv_a") = pybind11::none(), pybind11::arg("g_b") = pybind11::none(),
+        pybind11::arg("inv_b") = pybind11::none(), pybind11::arg("sink_ga") = pybind11::none(),
+        pybind11::arg("sink_ba") = pybind11::none(), pybind11::arg("sink_gb") = pybind11::none(),
+        pybind11::arg("sink_bb") = pybind11::none());
   m.def("bn_bwd_apply", &bn_bwd_apply, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
         pybind11::arg("ca"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("cb") = pybind11::none(),
         pybind11::arg("want_dz") = false, pybind11::arg("msc") = pybind11::none(),

@@ -45,22 +45,44 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
                              const float* in_shift = nullptr);
 
 // ---- BatchNorm (bn.hip) ---------------------------------------------------------
-hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s);
-hipError_t launch_bn_finalize(const double* sums, int C, double count, const float* gamma, const float* beta,
-                              float eps, float momentum, int update_running, float* running_mean, float* running_var,
-                              float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
+// Per-channel finalize (forward) and coefficient (backward) arguments, evaluated either by
+// their own kernels (SyncBN: after the cross-rank all-reduce of the sums) or inside the
+// last block of the single-launch column reduction (no cross-rank reduction needed).
+struct BnFinalizeArgs {
+  double count;
+  const float* gamma;
+  const float* beta;
+  float eps, momentum;
+  int update_running;
+  float* running_mean;
+  float* running_var;
+  float *scale, *shift, *mean, *invstd;
+};
+struct BnCoefArgs {
+  double count;
+  const float *g_a, *mean_a, *inv_a, *g_b, *mean_b, *inv_b;
+  float *coef_a, *coef_b, *dgamma_a, *dbeta_a, *dgamma_b, *dbeta_b;
+  int accumulate;
+};
+// Deterministic reduction of a [rows][nsets][C] fp32 slab to fp64 sums [nsets][C] in ONE
+// launch (per-block partials + last-arriver combine; no memset). epi: 0 sums only,
+// 1 + BN finalize (nsets 2), 2 + BN backward coefficients (nsets 2|3).
+int col_reduce_gy(int rows);
+hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, double* scratch, unsigned* counters,
+                             double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s);
+hipError_t launch_bn_finalize(const double* sums, int C, const BnFinalizeArgs& a, hipStream_t s);
 hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                                  float eps, float* scale, float* shift, hipStream_t s);
 hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, const void* r, const float* sc2,
                            const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s);
 int bn_bwd_reduce_blocks(long numel, int C);
+// partial [bn_bwd_reduce_blocks][nsets][C] written by the elementwise pass, then reduced
+// by launch_col_reduce (epi 0: sums only; epi 2: fused coefficients from `ca`)
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
-                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s,
+                                const float* mb, long numel, int C, float* partial, double* scratch,
+                                unsigned* counters, double* sums, int epi, const BnCoefArgs* ca, hipStream_t s,
                                 const float* msc = nullptr, const float* msh = nullptr);
-hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
-                              const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
-                              const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
-                              float* dgamma_b, float* dbeta_b, int accumulate, hipStream_t s);
+hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, const BnCoefArgs& a, hipStream_t s);
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
                                const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s,
                                const float* msc = nullptr, const float* msh = nullptr);

@@ -33,52 +33,119 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
 }
 
-// slab [rows][nsets][C] fp32 -> out [nsets][C] fp64 (out zeroed by the launcher); a 2-D
-// grid bounds the atomics per address to gridDim.y.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int rows, int nsets, int C,
-                                                          double* __restrict__ out) {
-  __shared__ double red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);   // index into [nsets][C]
-  const int ty = threadIdx.x >> 6;
-  double acc = 0.0;
-  if (col < nsets * C) {
-    const int which = col / C, ch = col % C;
-    for (int r = blockIdx.y * 4 + ty; r < rows; r += gridDim.y * 4)
-      acc += (double)slab[((size_t)r * nsets + which) * C + ch];
-  }
-  red[ty][threadIdx.x & 63] = acc;
-  __syncthreads();
-  if (ty == 0 && col < nsets * C) {
-    const double s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(out + col, s);
+// ---- per-channel epilogues (shared by the stand-alone kernels and the fused reduction) ----
+// (Σy, Σy²) over `count` rows -> scale/shift, mean/invstd (for backward), running stats
+// (unbiased variance, as torch BatchNorm2d)
+__device__ __forceinline__ void bn_finalize_one(int c, double s1, double s2, const BnFinalizeArgs& a) {
+  const double mean = s1 / a.count;
+  double var = s2 / a.count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  const float g = a.gamma ? a.gamma[c] : 1.f;
+  const float b = a.beta ? a.beta[c] : 0.f;
+  a.scale[c] = g * invstd;
+  a.shift[c] = b - (float)mean * g * invstd;
+  a.mean[c] = (float)mean;
+  a.invstd[c] = invstd;
+  if (a.update_running) {
+    const double unbiased = a.count > 1.0 ? var * a.count / (a.count - 1.0) : var;
+    a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * (float)mean;
+    a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * (float)unbiased;
   }
 }
 
-// sums [2][C] fp64 (Σy, Σy²) over `count` rows -> scale/shift (+ mean/invstd for bwd),
-// running stats update (unbiased var) when `update_running`.
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                   float momentum, int update_running, float* __restrict__ running_mean,
-                                   float* __restrict__ running_var, float* __restrict__ scale,
-                                   float* __restrict__ shift, float* __restrict__ mean_out,
-                                   float* __restrict__ invstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const double mean = sums[c] / count;
-  double var = sums[C + c] / count - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f;
-  const float b = beta ? beta[c] : 0.f;
-  scale[c] = g * invstd;
-  shift[c] = b - (float)mean * g * invstd;
-  mean_out[c] = (float)mean;
-  invstd_out[c] = invstd;
-  if (update_running) {
-    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+// sums: Σdz, Σdz·(ya−μa) [, Σdz·(yb−μb)] -> per-channel dy = A·dz + D·y + E and dγ/dβ
+// (accumulated into the parameter-gradient sinks when a.accumulate)
+__device__ __forceinline__ void bn_coef_one(int c, int C, const double* s, int nsets, const BnCoefArgs& a) {
+  const double sdz = s[0];
+  for (int set = 0; set < nsets; ++set) {
+    const float* gg = set == 0 ? a.g_a : a.g_b;
+    const float* mm = set == 0 ? a.mean_a : a.mean_b;
+    const float* iv = set == 0 ? a.inv_a : a.inv_b;
+    float* coef = set == 0 ? a.coef_a : a.coef_b;
+    const double sdzy = s[1 + set];
+    const double inv = iv[c], mu = mm[c], gam = gg ? gg[c] : 1.0;
+    const double A = gam * inv;
+    const double m1 = sdz / a.count, m2 = sdzy / a.count;
+    const double D = -A * inv * inv * m2;
+    const double E = -A * m1 - D * mu;
+    coef[c] = (float)A;
+    coef[C + c] = (float)D;
+    coef[2 * C + c] = (float)E;
+    float* dg = set == 0 ? a.dgamma_a : a.dgamma_b;
+    float* db = set == 0 ? a.dbeta_a : a.dbeta_b;
+    if (dg) dg[c] = (float)(sdzy * inv) + (a.accumulate ? dg[c] : 0.f);
+    if (db) db[c] = (float)sdz + (a.accumulate ? db[c] : 0.f);
   }
+}
+
+// slab [rows][NS][C] fp32 -> sums [NS][C] fp64 in one launch. grid (ceil(C/64), gy): block
+// (x, y) sums its contiguous row range for 64 channels (4 thread rows, fp64) into
+// scratch[y][NS][C]; it then takes an agent-scope ticket on counters[x], and the block that
+// draws gy-1 (after an acquire) adds the gy partials in fixed order — deterministic for any
+// dispatch order / XCD placement — writes the sums, runs the per-channel epilogue and
+// resets the counter for the next launch (counters are zeroed once at allocation).
+template <int NS, int EPI>
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                         double* scratch, unsigned* counters,
+                                                         double* __restrict__ sums, BnFinalizeArgs fa, BnCoefArgs ca) {
+  __shared__ double red[NS][4][64];
+  __shared__ int is_last;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int gy = gridDim.y;
+  const int per = (rows + gy - 1) / gy;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  double acc[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) acc[q] = 0.0;
+  if (c < C) {
+    for (int r = r0 + ty; r < r1; r += 4)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) acc[q] += (double)slab[((size_t)r * NS + q) * C + c];
+  }
+#pragma unroll
+  for (int q = 0; q < NS; ++q) red[q][ty][tx] = acc[q];
+  __syncthreads();
+  if (ty == 0 && c < C) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      scratch[((size_t)blockIdx.y * NS + q) * C + c] = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
+  }
+  if (gy > 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(counters + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = (t == (unsigned)gy - 1u);
+      if (is_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!is_last) return;
+  }
+  if (ty == 0 && c < C) {
+    double t[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) t[q] = 0.0;
+    for (int y = 0; y < gy; ++y)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) t[q] += scratch[((size_t)y * NS + q) * C + c];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) sums[(size_t)q * C + c] = t[q];
+    if (EPI == 1) bn_finalize_one(c, t[0], t[1], fa);
+    if (EPI == 2) bn_coef_one(c, C, t, NS - 1, ca);
+  }
+  if (gy > 1 && threadIdx.x == 0) __hip_atomic_store(counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int C, BnFinalizeArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) bn_finalize_one(c, sums[c], sums[C + c], a);
 }
 
 // eval-mode affine from running statistics
@@ -222,36 +289,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
 }
 
-// per-channel dy = A·dz + D·y + E, dγ, dβ from the reduced sums
-__global__ void bn_bwd_coef_kernel(const double* __restrict__ sums, int nsets, int C, double count,
-                                   const float* __restrict__ g_a, const float* __restrict__ mean_a,
-                                   const float* __restrict__ inv_a, const float* __restrict__ g_b,
-                                   const float* __restrict__ mean_b, const float* __restrict__ inv_b,
-                                   float* __restrict__ coef_a, float* __restrict__ coef_b,
-                                   float* __restrict__ dgamma_a, float* __restrict__ dbeta_a,
-                                   float* __restrict__ dgamma_b, float* __restrict__ dbeta_b, int accumulate) {
+__global__ void bn_bwd_coef_kernel(const double* __restrict__ sums, int nsets, int C, BnCoefArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double sdz = sums[c];
-  for (int set = 0; set < nsets; ++set) {
-    const float* gg = set == 0 ? g_a : g_b;
-    const float* mm = set == 0 ? mean_a : mean_b;
-    const float* iv = set == 0 ? inv_a : inv_b;
-    float* coef = set == 0 ? coef_a : coef_b;
-    const double sdzy = sums[(size_t)(1 + set) * C + c];
-    const double inv = iv[c], mu = mm[c], gam = gg ? gg[c] : 1.0;
-    const double A = gam * inv;
-    const double m1 = sdz / count, m2 = sdzy / count;
-    const double D = -A * inv * inv * m2;
-    const double E = -A * m1 - D * mu;
-    coef[c] = (float)A;
-    coef[C + c] = (float)D;
-    coef[2 * C + c] = (float)E;
-    float* dg = set == 0 ? dgamma_a : dgamma_b;
-    float* db = set == 0 ? dbeta_a : dbeta_b;
-    if (dg) dg[c] = (float)(sdzy * inv) + (accumulate ? dg[c] : 0.f);
-    if (db) db[c] = (float)sdz + (accumulate ? db[c] : 0.f);
-  }
+  double t[3];
+  for (int q = 0; q <= nsets; ++q) t[q] = sums[(size_t)q * C + c];
+  bn_coef_one(c, C, t, nsets, a);
 }
 
 template <bool TWO>
@@ -303,26 +346,35 @@ int ew_grid(long n8) {
 
 }  // namespace
 
-static hipError_t launch_slab_reduce(const float* slab, int rows, int nsets, int C, double* out, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(out, 0, sizeof(double) * nsets * C, s);
-  if (e != hipSuccess) return e;
-  int gy = (rows + 127) / 128;   // >= 32 rows per thread-row
+int col_reduce_gy(int rows) {
+  int gy = (rows + 31) / 32;   // >= 32 rows per block
   if (gy > 64) gy = 64;
   if (gy < 1) gy = 1;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((nsets * C + 63) / 64, gy), dim3(256), 0, s, slab, rows, nsets, C, out);
+  return gy;
+}
+
+hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, double* scratch, unsigned* counters,
+                             double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s) {
+  if (rows < 1 || C < 1 || (epi == 1 && (nsets != 2 || !fa)) || (epi == 2 && (nsets < 2 || !ca)))
+    return hipErrorInvalidValue;
+  const dim3 grid((C + 63) / 64, col_reduce_gy(rows)), blk(256);
+  const BnFinalizeArgs f = fa ? *fa : BnFinalizeArgs{};
+  const BnCoefArgs k = ca ? *ca : BnCoefArgs{};
+#define SDX_CR(NS, EPI) hipLaunchKernelGGL((col_reduce_kernel<NS, EPI>), grid, blk, 0, s, slab, rows, C, scratch, counters, sums, f, k)
+  if (nsets == 2) {
+    if (epi == 0) SDX_CR(2, 0); else if (epi == 1) SDX_CR(2, 1); else SDX_CR(2, 2);
+  } else if (nsets == 3) {
+    if (epi == 0) SDX_CR(3, 0); else SDX_CR(3, 2);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef SDX_CR
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
 
-hipError_t launch_bn_stats_reduce(const float* slab, int rows, int C, double* out, hipStream_t s) {
-  return launch_slab_reduce(slab, rows, 2, C, out, s);
-}
-
-hipError_t launch_bn_finalize(const double* sums, int C, double count, const float* gamma, const float* beta,
-                              float eps, float momentum, int update_running, float* running_mean, float* running_var,
-                              float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, C, count, gamma, beta, eps,
-                     momentum, update_running, running_mean, running_var, scale, shift, mean, invstd);
+hipError_t launch_bn_finalize(const double* sums, int C, const BnFinalizeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, C, a);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -362,7 +414,8 @@ int bn_bwd_reduce_blocks(long numel, int C) {
 }
 
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
-                                const float* mb, long numel, int C, float* partial, double* sums, hipStream_t s,
+                                const float* mb, long numel, int C, float* partial, double* scratch,
+                                unsigned* counters, double* sums, int epi, const BnCoefArgs* ca, hipStream_t s,
                                 const float* msc, const float* msh) {
   const int nsets = yb ? 3 : 2;
   const long n8 = numel / 8;
@@ -378,15 +431,11 @@ hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* 
                        (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)nullptr, (const float*)nullptr,
                        n8, C8, C, partial, msc, msh);
   SDX_LAUNCH_CHECK();
-  return launch_slab_reduce(partial, g, nsets, C, sums, s);
+  return launch_col_reduce(partial, g, nsets, C, scratch, counters, sums, epi, nullptr, ca, s);
 }
 
-hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, double count, const float* g_a,
-                              const float* mean_a, const float* inv_a, const float* g_b, const float* mean_b,
-                              const float* inv_b, float* coef_a, float* coef_b, float* dgamma_a, float* dbeta_a,
-                              float* dgamma_b, float* dbeta_b, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, nsets, C, count, g_a, mean_a,
-                     inv_a, g_b, mean_b, inv_b, coef_a, coef_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b, accumulate);
+hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, const BnCoefArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, nsets, C, a);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -42,13 +42,18 @@ class _BN:
     """Per-BN forward state: finalize (train) or eval affine."""
 
     @staticmethod
-    def forward(m, sums, bn, count, training, group):
+    def forward(m, slab, bn, count, training, group):
+        """``slab``: the conv epilogue's per-tile (Σy, Σy²). Single process: reduction +
+        finalize in one launch; SyncBN: reduce, fp64 all-reduce, finalize."""
         if training:
-            if group is not None:
-                dist.all_reduce(sums, group=group)
-            sc, sh, mean, inv = m.bn_finalize(sums, float(count), bn.weight.detach(), bn.bias.detach(), bn.eps,
-                                              bn.momentum if bn.momentum is not None else 0.1,
-                                              bn.track_running_stats, bn.running_mean, bn.running_var)
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            args = (float(count), bn.weight.detach(), bn.bias.detach(), bn.eps, mom, bn.track_running_stats,
+                    bn.running_mean, bn.running_var)
+            if group is None:
+                return tuple(m.bn_stats_finalize(slab, *args))
+            sums = m.bn_stats_reduce(slab)
+            dist.all_reduce(sums, group=group)
+            sc, sh, mean, inv = m.bn_finalize(sums, *args)
             return sc, sh, mean, inv
         sc, sh = m.bn_eval_affine(bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.eps)
         return sc, sh, None, None
@@ -59,7 +64,7 @@ def _conv(m, x, w, stride, pad, stats, in_bn=None):
     kernel feeds relu(x·scale + shift) to the GEMM."""
     isc, ish = in_bn if in_bn is not None else (None, None)
     y, slab = m.conv_fwd(x, w, stride, pad, stats, -1, isc, ish)
-    return y, (m.bn_stats_reduce(slab) if stats else None)
+    return y, (slab if stats else None)
 
 
 def _act(m, y, sc, sh):
@@ -74,17 +79,21 @@ def _bn_bwd(m, dout, out, y, mean, inv, bn, count, group, y_b=None, mean_b=None,
     """BN(+second BN)+ReLU backward with dγ/dβ written into the parameter sinks.
     ReLU mask from ``out``, or (``out`` None) from ``mask=(scale, shift)``: y·scale+shift > 0."""
     msc, msh = mask if (out is None and mask is not None) else (None, None)
-    s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b, msc, msh)
-    if group is not None:
+    snk = dict(sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias))
+    if y_b is not None:
+        snk.update(sink_gb=sinks.target(bn_b.weight), sink_bb=sinks.target(bn_b.bias))
+    gb = bn_b.weight.detach() if y_b is not None else None
+    if group is None:
+        # elementwise reduce + (last-block) coefficients: two launches, no host round trip
+        ca, cb, _, _, _, _ = m.bn_bwd_reduce_coef(dout, out, y, mean, y_b, mean_b, msc, msh, float(count),
+                                                  bn.weight.detach(), inv, gb, inv_b, **snk)
+    else:
+        s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b, msc, msh)
         dist.all_reduce(s, group=group)
+        ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, gb, mean_b, inv_b, **snk)
     if y_b is None:
-        ca, _, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv,
-                                          sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias))
         dya, _, dz = m.bn_bwd_apply(dout, out, y, ca, None, None, want_dz, msc, msh)
         return dya, None, dz
-    ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, bn_b.weight.detach(), mean_b,
-                                       inv_b, sink_ga=sinks.target(bn.weight), sink_ba=sinks.target(bn.bias),
-                                       sink_gb=sinks.target(bn_b.weight), sink_bb=sinks.target(bn_b.bias))
     dya, dyb, _ = m.bn_bwd_apply(dout, out, y, ca, y_b, cb, False)
     return dya, dyb, None
 

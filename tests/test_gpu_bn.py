@@ -102,3 +102,62 @@ def test_bn_bwd_mask_from_input(gpu):
     d_ref = m.bn_bwd_apply(dout, a, y, ca)[0]
     d = m.bn_bwd_apply(dout, None, y, ca, msc=sc, msh=sh)[0]
     assert _rel(d, d_ref) < 1e-2
+
+
+@pytest.mark.parametrize("rows,C", [(1, 64), (37, 128), (4096, 64), (300, 2048)])
+def test_single_launch_stats_finalize(gpu, rows, C):
+    """bn_stats_finalize (one launch: per-block partials + last-arriver combine) ==
+    bn_stats_reduce + bn_finalize == fp64 torch, bitwise-stable across repeated calls."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(2)
+    slab = torch.randn(rows, 2, C, device=gpu)
+    slab[:, 1] = slab[:, 1].abs() * 3 + slab[:, 0] ** 2
+    ref = slab.double().sum(0)
+    s = m.bn_stats_reduce(slab)
+    assert torch.allclose(s, ref, rtol=1e-12, atol=1e-9)
+    g, b = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    count = float(rows * 16)
+    rm1, rv1 = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    a = m.bn_finalize(s, count, g, b, 1e-5, 0.1, True, rm1, rv1)
+    outs = [m.bn_stats_finalize(slab, count, g, b, 1e-5, 0.1, True, rm2, rv2)]
+    for t, u in zip(a, outs[0]):
+        assert torch.equal(t, u)
+    assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+    for _ in range(3):   # counters reset by the last block: repeated launches stay exact
+        o = m.bn_stats_finalize(slab, count, g, b, 1e-5, 0.1, False, None, None)
+        for t, u in zip(a, o):
+            assert torch.equal(t, u)
+
+
+@pytest.mark.parametrize("two", [False, True])
+def test_bwd_reduce_coef_fused(gpu, two):
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(3)
+    N, H, W, C = 32, 16, 16, 64
+    y = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    y2 = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    out = torch.relu(torch.randn(N, H, W, C, device=gpu)).bfloat16()
+    dout = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    mu, inv = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    mu2, inv2 = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    g1, g2 = torch.rand(C, device=gpu) + 0.5, torch.rand(C, device=gpu) + 0.5
+    cnt = float(N * H * W)
+    yb, mb = (y2, mu2) if two else (None, None)
+    s = m.bn_bwd_reduce(dout, out, y, mu, yb, mb)
+    ref = m.bn_bwd_coef(s, cnt, g1, mu, inv, g2 if two else None, mb, inv2 if two else None)
+    for _ in range(2):
+        got = m.bn_bwd_reduce_coef(dout, out, y, mu, yb, mb, None, None, cnt, g1, inv, g2 if two else None,
+                                   inv2 if two else None)
+        for t, u in zip(ref, got):
+            assert torch.equal(t, u)
+    # sinks accumulate
+    sga, sba = torch.ones(C, device=gpu), torch.ones(C, device=gpu)
+    kw = dict(sink_ga=sga, sink_ba=sba)
+    if two:
+        kw.update(sink_gb=torch.ones(C, device=gpu), sink_bb=torch.ones(C, device=gpu))
+    m.bn_bwd_reduce_coef(dout, out, y, mu, yb, mb, None, None, cnt, g1, inv, g2 if two else None,
+                         inv2 if two else None, **kw)
+    assert torch.allclose(sga, ref[2] + 1) and torch.allclose(sba, ref[3] + 1)
