@@ -82,9 +82,12 @@ __device__ __forceinline__ void bn_coef_one(int c, int C, const double* s, int n
 // slab [rows][NS][C] fp32 -> sums [NS][C] fp64 in one launch. grid (ceil(C/64), gy): block
 // (x, y) sums its contiguous row range for 64 channels (4 thread rows, fp64) into
 // scratch[y][NS][C]; it then takes an agent-scope ticket on counters[x], and the block that
-// draws gy-1 (after an acquire) adds the gy partials in fixed order — deterministic for any
-// dispatch order / XCD placement — writes the sums, runs the per-channel epilogue and
-// resets the counter for the next launch (counters are zeroed once at allocation).
+// draws gy-1 adds the gy partials in fixed order — deterministic for any dispatch order /
+// XCD placement — writes the sums, runs the per-channel epilogue and resets the counter for
+// the next launch (counters are zeroed once at allocation). The partials are handed off
+// with write-through (sc1) stores and read back with sc1 loads, so no agent-scope release
+// fence is needed: such a fence would write back the whole L2 (still dirty with the
+// producing conv's output) in every block.
 template <int NS, int EPI>
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ slab, int rows, int C,
                                                          double* scratch, unsigned* counters,
@@ -100,41 +103,79 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
 #pragma unroll
   for (int q = 0; q < NS; ++q) acc[q] = 0.0;
   if (c < C) {
-    for (int r = r0 + ty; r < r1; r += 4)
+    // 4 rows per trip: 4·NS independent loads in flight per thread (latency-bound loop)
+    int r = r0 + ty;
+    for (; r + 12 < r1; r += 16) {
+      float v[4][NS];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) v[u][q] = slab[((size_t)(r + 4 * u) * NS + q) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) acc[q] += (double)v[u][q];
+    }
+    for (; r < r1; r += 4)
 #pragma unroll
       for (int q = 0; q < NS; ++q) acc[q] += (double)slab[((size_t)r * NS + q) * C + c];
   }
 #pragma unroll
   for (int q = 0; q < NS; ++q) red[q][ty][tx] = acc[q];
   __syncthreads();
+  unsigned long long* sc = reinterpret_cast<unsigned long long*>(scratch);
   if (ty == 0 && c < C) {
 #pragma unroll
-    for (int q = 0; q < NS; ++q)
-      scratch[((size_t)blockIdx.y * NS + q) * C + c] = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
+    for (int q = 0; q < NS; ++q) {
+      const double v = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
+      __hip_atomic_store(sc + ((size_t)blockIdx.y * NS + q) * C + c, (unsigned long long)__double_as_longlong(v),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 write-through
+    }
   }
   if (gy > 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every storing wave drains
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned t = __hip_atomic_fetch_add(counters + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       is_last = (t == (unsigned)gy - 1u);
-      if (is_last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
     }
     __syncthreads();
     if (!is_last) return;
   }
-  if (ty == 0 && c < C) {
+  // combine: thread row ty sums partials y = ty, ty+4, ... (all loads issued up front), then
+  // the 4 row sums are added in fixed order
+  {
     double t[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) t[q] = 0.0;
-    for (int y = 0; y < gy; ++y)
+    if (c < C) {
+      constexpr int MAXY = 16;   // gy <= 64
+      unsigned long long v[MAXY][NS];
 #pragma unroll
-      for (int q = 0; q < NS; ++q) t[q] += scratch[((size_t)y * NS + q) * C + c];
+      for (int k = 0; k < MAXY; ++k) {
+        const int y = ty + 4 * k;
+        if (y < gy) {
+#pragma unroll
+          for (int q = 0; q < NS; ++q)
+            v[k][q] = __hip_atomic_load(sc + ((size_t)y * NS + q) * C + c, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);   // sc1 loads
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < MAXY; ++k)
+        if (ty + 4 * k < gy)
+#pragma unroll
+          for (int q = 0; q < NS; ++q) t[q] += __longlong_as_double((long long)v[k][q]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NS; ++q) red[q][ty][tx] = t[q];
+    __syncthreads();
+  }
+  if (ty == 0 && c < C) {
+    double t[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) t[q] = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
 #pragma unroll
     for (int q = 0; q < NS; ++q) sums[(size_t)q * C + c] = t[q];
     if (EPI == 1) bn_finalize_one(c, t[0], t[1], fa);
@@ -347,7 +388,8 @@ int ew_grid(long n8) {
 }  // namespace
 
 int col_reduce_gy(int rows) {
-  int gy = (rows + 31) / 32;   // >= 32 rows per block
+  // balance the per-block row loop (rows/gy/4 trips) against the final combine (gy/4 loads)
+  int gy = (int)(sqrt((double)rows) / 2.0 + 0.5);
   if (gy > 64) gy = 64;
   if (gy < 1) gy = 1;
   return gy;
