@@ -48,6 +48,9 @@ struct IgemmParams {
   // WGRAD: B = x): x' = max(x·in_scale[c] + in_shift[c], 0); padding taps stay exactly 0
   const float* in_scale;
   const float* in_shift;
+  // diagnostic ablation (SDX_IGEMM_ABLATE bits, timing only — results are wrong):
+  // 1 skip LDS stores, 2 skip global loads, 4 skip MFMAs
+  int ablate;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -73,6 +76,15 @@ __device__ __forceinline__ int kout_off(int row, int ch) {
 }
 
 __device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// 16 zero bytes in global memory: out-of-bounds operand chunks (padding taps, tail rows,
+// K tail) load from here instead of being skipped, so every staging load is unconditional.
+// A predicated load makes hipcc branch around it and drain the whole load queue
+// (vmcnt(0)) before the LDS write, which defeats any prefetch depth.
+__device__ __attribute__((aligned(16))) uint16_t g_zero16[8];
+__device__ __forceinline__ uint4 ld16_or_zero(const uint16_t* p, bool ok) {
+  return ld16(ok ? p : g_zero16);
+}
 
 // relu(x·s + t) on 8 packed bf16 channels (fp32 math, one rounding: same as bn_apply)
 __device__ __forceinline__ uint4 bnrelu8(uint4 v, const float (&s)[8], const float (&t)[8]) {
@@ -103,7 +115,7 @@ struct Tile {
   static constexpr int B_CH = BN * BK / 8 / 256;
 };
 
-template <int MODE, int BM, int BN, int WM, int WN>
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   using T = Tile<MODE, BM, BN>;
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
@@ -201,16 +213,25 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     load8f(p.in_shift + wb_c, wsh);
   }
 
-  uint4 ra[T::A_CH], rb[T::B_CH];
-  // fused BN+ReLU prologue: applied when the staged registers are written to LDS (after the
-  // MFMAs of the current tile), never right after the global load — that would put the
-  // load latency back on the critical path. Bit i of ld_mask = chunk i was loaded in-bounds
-  // (padding taps / tail rows stay exactly 0).
+  // One register stage: the tile's operand chunks in flight from global memory. The fused
+  // BN+ReLU prologue is applied when a stage is written to LDS (after the MFMAs of the
+  // current tile), never right after the global load — that would put the load latency
+  // back on the critical path. Bit i of ld_mask = chunk i was loaded in-bounds (padding
+  // taps / tail rows stay exactly 0).
+  struct Stage {
+    uint4 ra[T::A_CH], rb[T::B_CH];
+    unsigned ld_mask;
+    float isc[8], ish[8];
+  };
   const bool bn_in = (MODE == MODE_FWD) && p.in_scale != nullptr;
-  float isc[8], ish[8];
-  unsigned ld_mask = 0;
 
-  auto load_tile = [&](int k0) {
+  auto load_tile = [&](int k0, Stage& st) {
+    if (p.ablate & 2) return;
+    uint4 (&ra)[T::A_CH] = st.ra;
+    uint4 (&rb)[T::B_CH] = st.rb;
+    unsigned& ld_mask = st.ld_mask;
+    float (&isc)[8] = st.isc;
+    float (&ish)[8] = st.ish;
     if (MODE == MODE_FWD || MODE == MODE_DGRAD) {
       // A: gather 8 consecutive k (same tap, 8 channels) for each owned row
       const int k = k0 + kin_ch * 8;
@@ -222,36 +243,28 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
       }
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (kok) {
-          if (MODE == MODE_FWD) {
-            if (is1x1) {
-              if (a_y[i] >= 0) {
-                v = ld16(p.a + a_base[i] + kc);
-                ld_mask |= 1u << i;
-              }
-            } else {
-              const int yy = a_y[i] + kr, xx = a_x[i] + ks;
-              if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W) {
-                v = ld16(p.a + a_base[i] + (kr * g.W + ks) * g.C + kc);
-                ld_mask |= 1u << i;
-              }
-            }
+        bool ok;
+        int off;
+        if (MODE == MODE_FWD) {
+          if (is1x1) {
+            ok = kok && a_y[i] >= 0;
+            off = a_base[i] + kc;
           } else {
-            const int ty = a_y[i] - kr, tx = a_x[i] - ks;
-            if ((unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q)
-              v = ld16(p.a + a_base[i] + (ty * g.Q + tx) * g.K + kc);
+            const int yy = a_y[i] + kr, xx = a_x[i] + ks;
+            ok = kok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
+            off = a_base[i] + (kr * g.W + ks) * g.C + kc;
           }
+          if (ok) ld_mask |= 1u << i;
+        } else {
+          const int ty = a_y[i] - kr, tx = a_x[i] - ks;
+          ok = kok && (unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q;
+          off = a_base[i] + (ty * g.Q + tx) * g.K + kc;
         }
-        ra[i] = v;
+        ra[i] = ld16_or_zero(p.a + off, ok);
       }
       // B: weights [Ncol][Kdim] K-contiguous
 #pragma unroll
-      for (int i = 0; i < T::B_CH; ++i) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (kok && b_off[i] >= 0) v = ld16(p.b + b_off[i] + k);
-        rb[i] = v;
-      }
+      for (int i = 0; i < T::B_CH; ++i) rb[i] = ld16_or_zero(p.b + b_off[i] + k, kok && b_off[i] >= 0);
       // advance the k decode by one tile
       kc += BK;
       while (kc >= cdim) {
@@ -265,9 +278,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         const int e = tid + 256 * i;
         const int row = e / A_CPR, ch = e % A_CPR;
         const int kk = k0 + row, co = m0 + ch * 8;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (kk < k_end && co < p.M) v = ld16(p.a + kk * g.K + co);
-        ra[i] = v;
+        ra[i] = ld16_or_zero(p.a + kk * g.K + co, kk < k_end && co < p.M);
       }
       // WGRAD B: im2col(x) rows (pixels) x BN (r,s,ci); the column chunk is fixed per thread
       if (wb_bn) ld_mask = 0;
@@ -276,29 +287,32 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         const int e = tid + 256 * i;
         const int row = e / B_CPR;
         const int kk = k0 + row;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (wb_ok && kk < k_end) {
-          if (is1x1) {
-            v = ld16(p.b + kk * g.C + wb_c);
-            ld_mask |= 1u << i;
-          } else {
-            const int n = (int)fdiv((unsigned)kk, p.div_pq);
-            const int rem = kk - n * g.P * g.Q;
-            const int pp = (int)fdiv((unsigned)rem, p.div_q);
-            const int qq = rem - pp * g.Q;
-            const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
-            if ((unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W) {
-              v = ld16(p.b + ((n * g.H + yy) * g.W + xx) * g.C + wb_c);
-              ld_mask |= 1u << i;
-            }
-          }
+        bool ok = wb_ok && kk < k_end;
+        int off;
+        if (is1x1) {
+          off = kk * g.C + wb_c;
+        } else {
+          const int n = (int)fdiv((unsigned)kk, p.div_pq);
+          const int rem = kk - n * g.P * g.Q;
+          const int pp = (int)fdiv((unsigned)rem, p.div_q);
+          const int qq = rem - pp * g.Q;
+          const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
+          ok = ok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
+          off = ((n * g.H + yy) * g.W + xx) * g.C + wb_c;
         }
-        rb[i] = v;
+        if (ok) ld_mask |= 1u << i;
+        rb[i] = ld16_or_zero(p.b + off, ok);
       }
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, Stage& st) {
+    if (p.ablate & 1) return;
+    uint4 (&ra)[T::A_CH] = st.ra;
+    uint4 (&rb)[T::B_CH] = st.rb;
+    const unsigned ld_mask = st.ld_mask;
+    const float (&isc)[8] = st.isc;
+    const float (&ish)[8] = st.ish;
     unsigned char* sa = smem + buf * T::STAGE;
     unsigned char* sb = sa + T::A_BYTES;
     if (bn_in) {
@@ -358,15 +372,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     return f;
   };
 
-  if (nk > 0) {
-    load_tile(k_begin);
-    store_tile(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load_tile(k_begin + (kt + 1) * BK);
+  auto compute = [&](int buf) {
+    if (p.ablate & 4) return;
     const unsigned char* sa = smem + buf * T::STAGE;
     const unsigned char* sb = sa + T::A_BYTES;
 #pragma unroll
@@ -389,8 +396,51 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (more) store_tile(buf ^ 1);
+  };
+
+  // K loop: two LDS buffers, one barrier per K-tile. DEPTH 1: the loads of tile k+1 are in
+  // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
+  // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
+  // issued a whole K-tile earlier (load latency covered by two tiles of MFMA work).
+  if (DEPTH == 1) {
+    Stage s0;
+    if (nk > 0) {
+      load_tile(k_begin, s0);
+      store_tile(0, s0);
+    }
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      const bool more = kt + 1 < nk;
+      load_tile(k_begin + (kt + 1) * BK, s0);   // past the end: zero-page loads (uniform vmcnt)
+      compute(buf);
+      if (more) store_tile(buf ^ 1, s0);
+      __syncthreads();
+    }
+  } else {
+    Stage s0, s1;
+    if (nk > 0) {
+      load_tile(k_begin, s0);
+      store_tile(0, s0);
+    }
+    load_tile(k_begin + BK, s1);
+    __syncthreads();
+    // prefetch loads are issued unconditionally (past the end they read the zero page):
+    // a conditional load block makes hipcc assume the shortest load queue and wait for
+    // the loads just issued before the LDS write
+    for (int kt = 0; kt < nk; kt += 2) {
+      // buffer 0 holds tile kt; s1 carries tile kt+1
+      load_tile(k_begin + (kt + 2) * BK, s0);
+      compute(0);
+      if (kt + 1 < nk) store_tile(1, s1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      // buffer 1 holds tile kt+1; s0 carries tile kt+2
+      load_tile(k_begin + (kt + 3) * BK, s1);
+      compute(1);
+      if (kt + 2 < nk) store_tile(0, s0);
+      __syncthreads();
+    }
   }
 
   // ---------------------------------- epilogues ----------------------------------
@@ -468,8 +518,9 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   }
 
   if (MODE == MODE_FWD && p.stats != nullptr) {
-    // per-column (Σy, Σy²) over this tile's rows (rows past M are exact zeros: their A rows
-    // were zero-filled), from the rounded values; one slab row per M-tile.
+    // per-column (Σy, Σy²) over this tile's rows, from the fp32 accumulators (rows past M
+    // are exact zeros: their A rows were zero-filled); one slab row per M-tile. Rows are
+    // reduced in registers over i, then over the 16 lanes c with DPP row adds.
     float s1[TN][4], s2[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -478,23 +529,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         float a1 = 0.f, a2 = 0.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const uint32_t w = (r < 2) ? ov[i][j].x : ov[i][j].y;
-          const float v = __uint_as_float((r & 1) ? (w & 0xffff0000u) : (w << 16));
+          const float v = acc[i][j][r];
           a1 += v;
-          a2 += v * v;
+          a2 = fmaf(v, v, a2);
         }
-        s1[j][r] = a1;
-        s2[j][r] = a2;
+        s1[j][r] = row16_sum(a1);
+        s2[j][r] = row16_sum(a2);
       }
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s1[j][r] += __shfl_xor(s1[j][r], off, 64);
-          s2[j][r] += __shfl_xor(s2[j][r], off, 64);
-        }
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);   // [WM][2][BN]
     if (c == 0) {
@@ -556,12 +597,40 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// register-prefetch depth of the K loop (SDX_IGEMM_DEPTH=1|2, default 2)
+int igemm_depth() {
+  static const int d = [] {
+    const char* e = getenv("SDX_IGEMM_DEPTH");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return d;
+}
+
+int igemm_ablate() {
+  static const int a = [] {
+    const char* e = getenv("SDX_IGEMM_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  return a;
+}
+
 template <int MODE, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
+  p.ablate = igemm_ablate();
   p.m_tiles = (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
   const int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), dim3(grid), dim3(256), 0, s, p);
+  // depth 2 only where the second register stage fits without spilling (checked with
+  // -Rpass-analysis=kernel-resource-usage)
+  constexpr bool kDepth2 = (BM == 64 && BN == 64) || (MODE == MODE_FWD && BM != 256);
+  if constexpr (kDepth2) {
+    if (igemm_depth() == 2) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2>), dim3(grid), dim3(256), 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+  }
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 1>), dim3(grid), dim3(256), 0, s, p);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
