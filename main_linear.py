@@ -4,6 +4,7 @@ python main_linear.py --learning_rate 5 --batch_size 256 --ckpt path/to/last.pth
 """
 from simclr_pytorch_distributed_amd.config import parse_linear
 from simclr_pytorch_distributed_amd.engine.linear import LinearEngine
+from simclr_pytorch_distributed_amd.utils.faults import guarded_main
 
 
 def main(argv=None):
@@ -12,4 +13,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    guarded_main(main)

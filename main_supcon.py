@@ -8,6 +8,7 @@ CPU:          python main_supcon.py --backend torch --dist_backend gloo --batch_
 """
 from simclr_pytorch_distributed_amd.config import parse_pretrain
 from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+from simclr_pytorch_distributed_amd.utils.faults import guarded_main
 
 
 def main(argv=None):
@@ -17,4 +18,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    guarded_main(main)

@@ -28,6 +28,7 @@ from ..optim.schedules import adjust_learning_rate, warmup_learning_rate
 from ..parallel import comm
 from ..utils.logging import setup_logging
 from ..utils.meters import AverageMeter, accuracy
+from ..utils.profiling import PhaseTimer
 from . import checkpoint as ckpt_mod
 from .pretrain import resolve_backend, step_seed
 
@@ -35,7 +36,7 @@ from .pretrain import resolve_backend, step_seed
 class LinearEngine:
     def __init__(self, opt, device: Optional[torch.device] = None, model: Optional[torch.nn.Module] = None):
         self.opt = opt
-        rank, local_rank, world, dev = comm.init_distributed(opt.dist_backend, device=device)
+        rank, local_rank, world, dev = comm.init_distributed(opt.dist_backend, getattr(opt, "comm_timeout", 600.0), device=device)
         self.device = dev
         setup_logging(opt.save_folder, rank)
         logging.info(f"create {opt.conf_work_path} ...")
@@ -70,6 +71,7 @@ class LinearEngine:
         self.aug_val = AugConfig.evaluation(32, opt.mean_t, opt.std_t)
         from ..utils.tb import Logger
         self.logger = Logger(opt.tb_folder, flush_secs=2)
+        self.prof = PhaseTimer(getattr(opt, "profile", False), dev)
 
     def _features(self, x):
         if self.backend == "torch":
@@ -90,17 +92,21 @@ class LinearEngine:
             if idx_i >= iters:
                 break
             dtm.update(time.time() - end)
-            x = augment(self.tr_x, idx, self.aug_train, step_seed(opt.seed, epoch, idx_i, 0))
-            labels = self.tr_y[idx]
+            ph = self.prof.phase
+            with ph("augment"):
+                x = augment(self.tr_x, idx, self.aug_train, step_seed(opt.seed, epoch, idx_i, 0))
+                labels = self.tr_y[idx]
             bsz = labels.shape[0]
             warmup_learning_rate(opt, epoch, idx_i, iters, self.optimizer)
-            feats = self._features(x)
-            output = self.classifier(feats.detach())
-            loss = self.criterion(output, labels)
-            acc1, acc5 = accuracy(output, labels, topk=(1, 5))
-            self.optimizer.zero_grad()
-            loss.backward()
-            self.optimizer.step()
+            with ph("encoder"):
+                feats = self._features(x)
+            with ph("classifier"):
+                output = self.classifier(feats.detach())
+                loss = self.criterion(output, labels)
+                acc1, acc5 = accuracy(output, labels, topk=(1, 5))
+                self.optimizer.zero_grad()
+                loss.backward()
+                self.optimizer.step()
             if (idx_i + 1) % opt.print_freq == 0 or idx_i + 1 == iters:
                 losses.update(loss.item(), bsz)
                 top1.update(acc1[0].item(), bsz)
@@ -110,6 +116,8 @@ class LinearEngine:
                              "DT {dt.val:.3f} ({dt.avg:.3f})\tloss {loss.val:.3f} ({loss.avg:.3f})\t"
                              "Acc@1 {top1.val:.3f} ({top1.avg:.3f})".format(
                                  epoch, idx_i + 1, iters, bt=bt, dt=dtm, loss=losses, top1=top1))
+                if self.prof.enabled:
+                    logging.info("phases (ms/step): " + PhaseTimer.format(self.prof.summary()))
                 sys.stdout.flush()
             end = time.time()
         return losses.avg, top1.avg, top5.avg

@@ -41,6 +41,8 @@ from ..parallel import comm
 from ..parallel.ddp import GradBucketReducer
 from ..utils.logging import setup_logging
 from ..utils.meters import AverageMeter
+from ..utils.faults import maybe_inject
+from ..utils.profiling import PhaseTimer
 from . import checkpoint as ckpt_mod
 
 
@@ -63,7 +65,7 @@ def step_seed(base: int, epoch: int, idx: int, rank: int) -> int:
 class PretrainEngine:
     def __init__(self, opt, device: Optional[torch.device] = None):
         self.opt = opt
-        rank, local_rank, world, dev = comm.init_distributed(opt.dist_backend, device=device)
+        rank, local_rank, world, dev = comm.init_distributed(opt.dist_backend, getattr(opt, "comm_timeout", 600.0), device=device)
         self.rank, self.world, self.device = rank, world, dev
         if opt.ngpu != world and world > 1:
             logging.warning(f"--ngpu {opt.ngpu} != launcher WORLD_SIZE {world}; using {world}")
@@ -118,6 +120,7 @@ class PretrainEngine:
         self._ramp_t = torch.zeros((), device=dev)
         self._graph = None
         self._graph_stats = None
+        self.prof = PhaseTimer(getattr(opt, "profile", False), dev)
         if getattr(opt, "resume", ""):
             self._resume(opt.resume)
 
@@ -164,21 +167,29 @@ class PretrainEngine:
         """Device work of one step: no host syncs, no host-dependent control flow
         (capturable into a hipGraph)."""
         opt = self.opt
-        x = self.make_views(idx, epoch, it)
-        labels = self.labels[idx]
-        feats = self.runner.forward(x)
-        loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
-        stats = self._norm_terms(feats)
-        loss = loss + stats.pop("extra_loss")
-        self.optimizer.zero_grad()
-        loss.backward()
+        ph = self.prof.phase
+        with ph("augment"):
+            x = self.make_views(idx, epoch, it)
+            labels = self.labels[idx]
+        with ph("forward"):
+            feats = self.runner.forward(x)
+        with ph("loss"):
+            loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
+            stats = self._norm_terms(feats)
+            loss = loss + stats.pop("extra_loss")
+        with ph("backward"):
+            self.optimizer.zero_grad()
+            loss.backward()
         if self.reducer is not None:
-            self.reducer.finish()
-        self.optimizer.step()
+            with ph("grad_sync_wait"):
+                self.reducer.finish()
+        with ph("optimizer"):
+            self.optimizer.step()
         stats["loss_local"] = loss.detach()
         return stats
 
     def train_step(self, idx: torch.Tensor, epoch: int, it: int, iters: int):
+        maybe_inject(self.rank, self.global_step)
         self._host_prelude(epoch, it, iters)
         if self._graph is not None:
             self._idx_buf.copy_(idx, non_blocking=True)
@@ -299,6 +310,8 @@ class PretrainEngine:
                             epoch, it + 1, iters, bt=dt, bta=batch_time.avg, dtv=data_time.val, dta=data_time.avg,
                             lv=v[6], la=losses.avg, nm=v[1], rec=v[2], var=v[3],
                             ips=opt.batch_size / max(dt, 1e-9)))
+                    if self.prof.enabled:
+                        logging.info("phases (ms/step): " + PhaseTimer.format(self.prof.summary()))
                     sys.stdout.flush()
                 window_loss = torch.zeros((), device=self.device)
                 window_n = 0
