@@ -54,6 +54,10 @@ class GradBucketReducer:
         self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (self.is_cuda and self.enabled) else None
         self._hooks = []
         self._index = {id(p): i for i, p in enumerate(flat.params)}
+        # a parameter is counted once per backward: fused blocks notify through their gradient
+        # sink AND autograd still runs the parameter's AccumulateGrad node (with a None grad),
+        # which fires the post-accumulate hook a second time
+        self._seen = [False] * len(flat.params)
         self._listener = None
         if self.enabled:
             for i, p in enumerate(flat.params):
@@ -82,6 +86,9 @@ class GradBucketReducer:
     # ---- backward -----------------------------------------------------------------
     def _make_hook(self, i):
         def hook(_p):
+            if self._seen[i]:
+                return
+            self._seen[i] = True
             b = self.buckets[self.bucket_of[i]]
             b["ready"] += 1
             if b["ready"] == len(b["params"]):
@@ -116,6 +123,7 @@ class GradBucketReducer:
             b["work"].wait()
             b["work"] = None
             b["ready"] = 0
+        self._seen = [False] * len(self._seen)
         if self.comm_stream is not None:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
 

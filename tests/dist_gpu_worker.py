@@ -1,0 +1,58 @@
+"""Worker for tests/test_gpu_dist.py: one native training step on cuda:0 as rank RANK of
+WORLD_SIZE (gloo carries the collectives, so several ranks can share the one GPU of the
+test box). Writes the updated flat parameters and BN running stats to OUT_DIR."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def main():
+    out_dir = sys.argv[1]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    from simclr_pytorch_distributed_amd.models.executor import to_nhwc_input
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    B = 16                                    # images per rank
+    G = 32                                    # global images
+    argv = ["--model", "resnet18", "--backend", "native", "--dist_backend", "gloo", "--synthetic",
+            "--synthetic_size", "64", "--learning_rate", "0.05", "--grad_semantics", "exact",
+            "--work_dir", out_dir, "--batch_size", str(G), "--ngpu", str(world)]
+    if world > 1:
+        argv.append("--syncBN")
+    opt = parse_pretrain(argv, make_dirs=False)
+    eng = PretrainEngine(opt, device=torch.device("cuda:0"))
+    torch.manual_seed(123)
+    init = SupConResNet("resnet18").state_dict()
+    eng.model.load_state_dict(init)
+    eng.model.train()
+    g = torch.Generator().manual_seed(7)
+    imgs = torch.randn(2, G, 3, 32, 32, generator=g)          # [view][global batch]
+    per = G // world
+    sl = slice(rank * per, (rank + 1) * per)
+    x = torch.cat([imgs[0, sl], imgs[1, sl]]).cuda()
+    feats = eng.runner.forward(to_nhwc_input(x))
+    loss = eng.criterion(feats)
+    eng.optimizer.zero_grad()
+    loss.backward()
+    if eng.reducer is not None:
+        eng.reducer.finish()
+    grad = eng.flat.grad.detach().clone()
+    eng.optimizer.step()
+    torch.cuda.synchronize()
+    bn = eng.model.encoder.layer1[0].bn1
+    torch.save({"flat": eng.flat.flat.detach().cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
+                "loss": float(loss.detach()), "grad": grad.cpu(), "names": list(eng.flat.names),
+                "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"w{world}_r{rank}.pt"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

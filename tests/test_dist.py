@@ -163,3 +163,45 @@ def _init_state():
 @pytest.mark.slow
 def test_two_rank_step_equals_single_rank():
     _run(_step_case, 2)
+
+
+def _sink_case(rank, world, d):  # noqa: C901
+    """Fused-style parameters (gradient written into the sink + sinks.notify, autograd still
+    runs their AccumulateGrad with a None grad) are counted ONCE by the bucket reducer: the
+    bucket must not be launched before the last parameter's gradient is written."""
+    from simclr_pytorch_distributed_amd.ops import sinks
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    from simclr_pytorch_distributed_amd.parallel.ddp import GradBucketReducer
+
+    class Fused(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, *ps):
+            ctx.ps = ps
+            return x * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            for p in ctx.ps:
+                sinks.target(p).add_(float(rank + 1))
+            done.append(1)
+            sinks.notify(ctx.ps)
+            return (g * 2,) + (None,) * len(ctx.ps)
+
+    m = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+    flat = FlatParams(m)
+    red = GradBucketReducer(flat, bucket_mb=64)            # ONE bucket spanning both Functions
+    assert len(red.buckets) == 1
+    done, at_launch = [], []
+    orig = red._launch
+    red._launch = lambda b: (at_launch.append(len(done)), orig(b))[1]
+    x = torch.randn(2, 4, requires_grad=True)
+    y = Fused.apply(Fused.apply(x, *m[0].parameters()), *m[1].parameters())
+    y.sum().backward()
+    assert at_launch == [2], at_launch                     # launched once, after BOTH backwards
+    red.finish()
+    for p in m.parameters():
+        assert torch.allclose(p.grad, torch.full_like(p, sum(r + 1 for r in range(world))))
+
+
+def test_reducer_counts_sink_params_once():
+    _run(_sink_case, 2)

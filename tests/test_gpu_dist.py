@@ -1,0 +1,61 @@
+"""The distributed native path on ONE GPU: 2 ranks (gloo collectives on GPU tensors,
+both processes on cuda:0) — SyncBN through the fused blocks, row-owned contrastive loss
+with gathered negatives, bucketed gradient reduction on the comm stream, fused SGD —
+must reproduce the single-rank step on the concatenated batch (exact gradient
+semantics), up to bf16 reduction-order noise."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(world, out):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        try:
+            _, err = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("distributed worker timed out")
+        assert p.returncode == 0, err[-3000:]
+
+
+def test_two_rank_native_step_equals_single_rank(gpu, tmp_path):
+    _launch(1, tmp_path)
+    _launch(2, tmp_path)
+    ref = torch.load(tmp_path / "w1_r0.pt", weights_only=True)
+    a = torch.load(tmp_path / "w2_r0.pt", weights_only=True)
+    b = torch.load(tmp_path / "w2_r1.pt", weights_only=True)
+    bad = [n for n, o, k in zip(a["names"], a["offsets"], a["numels"])
+           if not torch.equal(a["grad"][o:o + k], b["grad"][o:o + k])]
+    assert not bad, f"all-reduced gradients differ across ranks for {len(bad)} params: {bad[:12]}"
+    assert torch.equal(a["flat"], b["flat"])                  # replicas stay identical
+    assert torch.equal(a["rm"], b["rm"])                      # SyncBN running stats identical
+    init = torch.load(tmp_path / "w1_r0.pt", weights_only=True)
+    d_ref = ref["flat"] - a["flat"]
+    rel = d_ref.norm() / (ref["flat"].norm() + 1e-12)
+    assert rel < 2e-3, float(rel)
+    assert torch.allclose(a["rm"], ref["rm"], rtol=1e-2, atol=1e-3)
+    # global loss = sum of the ranks' row-owned losses
+    assert abs(a["loss"] + b["loss"] - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3
