@@ -62,7 +62,10 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 // K-inner image: [rows][BK] bf16, 128-B rows; 16-B chunk swizzle conflict-free for 16 rows.
 __device__ __forceinline__ int kin_off(int row, int ch) {
-  return row * (BK * 2) + ((ch ^ ((row >> 1) & 7)) << 4);
+  // XOR swizzle by row&7: conflict-free for the fragment ds_read_b128 lane groups, and an
+  // 8-row x 128-B block stays one contiguous 1 KiB piece in which lane L of a
+  // global_load_lds instruction always carries logical chunk (L&7)^(L>>3)
+  return row * (BK * 2) + ((ch ^ (row & 7)) << 4);
 }
 
 // K-outer image: [BK][COLS] bf16; chunk swizzle keeps the transposed reads of a 32-lane
@@ -115,6 +118,10 @@ struct Tile {
   static constexpr int B_CH = BN * BK / 8 / 256;
 };
 
+// DEPTH: 1 / 2 = register-staged operands, 1 or 2 K-tiles of prefetch; 3 = LDS-DMA
+// (global_load_lds) staging of both K-inner operands (FWD / DGRAD without the BN prologue):
+// no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
+// LDS resource of the register-staged loop.
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   using T = Tile<MODE, BM, BN>;
@@ -144,9 +151,16 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   const int nk = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
 
   // ---- per-thread loader state (32-bit address math: tensors < 2^31 elements) ----
-  // K-inner operands: thread owns chunk column ch = tid % 8 and rows tid/8 + 32*i.
-  const int kin_ch = tid & 7;
+  // K-inner operands. Register staging: thread owns chunk column ch = tid % 8 and rows
+  // tid/8 + 32*i. LDS-DMA: instruction i of wave w fills rows 8*(w*CH + i) .. +7 (1 KiB),
+  // lane L row +L/8 at physical chunk L%8, i.e. logical chunk (L&7)^(L>>3).
+  constexpr bool GL = DEPTH == 3;
+  static_assert(!GL || MODE != MODE_WGRAD, "LDS-DMA staging covers the K-inner operands");
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int kin_ch = GL ? ((lane & 7) ^ ((lane >> 3) & 7)) : (tid & 7);
   const int kin_row0 = tid >> 3;
+  auto a_row = [&](int i) { return GL ? 8 * (wvu * T::A_CH + i) + (lane >> 3) : kin_row0 + 32 * i; };
+  auto b_row = [&](int i) { return GL ? 8 * (wvu * T::B_CH + i) + (lane >> 3) : kin_row0 + 32 * i; };
   const bool is1x1 = (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
   // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
   // tap; DGRAD: dy coordinate of tap (r0, s0))
@@ -161,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     const int wdim = (MODE == MODE_FWD) ? g.Q : p.Wc;
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
-      const int m = m0 + kin_row0 + 32 * i;
+      const int m = m0 + a_row(i);
       if (m < p.M) {
         const int n = m / hw_out, rem = m - n * hw_out;
         const int yy = rem / wdim, xx = rem - yy * wdim;
@@ -183,7 +197,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     }
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
-      const int col = n0 + kin_row0 + 32 * i;
+      const int col = n0 + b_row(i);
       b_off[i] = col < p.Ncol ? col * p.Kdim : -1;
     }
     const int k = k_begin + kin_ch * 8;
@@ -306,6 +320,50 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     }
   };
 
+  // LDS-DMA staging of one K-tile into LDS buffer `buf` (out-of-range chunks copy the zero page)
+  auto issue_glds = [&](int k0, int buf) {
+    unsigned char* sa = smem + buf * T::STAGE;
+    unsigned char* sb = sa + T::A_BYTES;
+    const int k = k0 + kin_ch * 8;
+    const bool kok = k < k_end;
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i) {
+      bool ok;
+      int off;
+      if (MODE == MODE_FWD) {
+        if (is1x1) {
+          ok = kok && a_y[i] >= 0;
+          off = a_base[i] + kc;
+        } else {
+          const int yy = a_y[i] + kr, xx = a_x[i] + ks;
+          ok = kok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
+          off = a_base[i] + (kr * g.W + ks) * g.C + kc;
+        }
+      } else {
+        const int ty = a_y[i] - kr, tx = a_x[i] - ks;
+        ok = kok && (unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q;
+        off = a_base[i] + (ty * g.Q + tx) * g.K + kc;
+      }
+      const uint16_t* src = ok ? p.a + off : g_zero16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_CH; ++i) {
+      const bool ok = kok && b_off[i] >= 0;
+      const uint16_t* src = ok ? p.b + b_off[i] + k : g_zero16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
+                                       16, 0, 0);
+    }
+    kc += BK;
+    while (kc >= cdim) {
+      kc -= cdim;
+      if (++ks == tap_s) { ks = 0; ++kr; }
+    }
+  };
+
   auto store_tile = [&](int buf, Stage& st) {
     if (p.ablate & 1) return;
     uint4 (&ra)[T::A_CH] = st.ra;
@@ -402,7 +460,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
   // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
   // issued a whole K-tile earlier (load latency covered by two tiles of MFMA work).
-  if (DEPTH == 1) {
+  if (DEPTH == 3) {
+    // the DMA of tile k+1 overlaps the MFMAs of tile k; the barrier's vmcnt(0) lands it
+    if (nk > 0) issue_glds(k_begin, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) issue_glds(k_begin + (kt + 1) * BK, buf ^ 1);
+      compute(buf);
+      __syncthreads();
+    }
+  } else if (DEPTH == 1) {
     Stage s0;
     if (nk > 0) {
       load_tile(k_begin, s0);
@@ -606,6 +674,15 @@ int igemm_depth() {
   return d;
 }
 
+// LDS-DMA operand staging for FWD/DGRAD (SDX_IGEMM_GLDS=0 disables)
+int igemm_glds() {
+  static const int a = [] {
+    const char* e = getenv("SDX_IGEMM_GLDS");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return a;
+}
+
 int igemm_ablate() {
   static const int a = [] {
     const char* e = getenv("SDX_IGEMM_ABLATE");
@@ -623,6 +700,13 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   // depth 2 only where the second register stage fits without spilling (checked with
   // -Rpass-analysis=kernel-resource-usage)
   constexpr bool kDepth2 = (BM == 64 && BN == 64) || (MODE == MODE_FWD && BM != 256);
+  if constexpr (MODE != MODE_WGRAD) {
+    if (p.in_scale == nullptr && igemm_glds()) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 3>), dim3(grid), dim3(256), 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+  }
   if constexpr (kDepth2) {
     if (igemm_depth() == 2) {
       hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2>), dim3(grid), dim3(256), 0, s, p);
