@@ -3,6 +3,7 @@
 #include "ops_decl.h"
 #include "launchers.h"
 
+#include <cmath>
 #include <map>
 #include <mutex>
 
@@ -37,17 +38,30 @@ void in_bn_ptrs(const OptT& sc, const OptT& sh, int64_t C, const float** ps, con
   TORCH_CHECK((*ps == nullptr) == (*pt == nullptr), "in_scale and in_shift must be given together");
 }
 
-// Pick the tile config minimising padded work, with a mild preference for the larger
-// (more MFMA-efficient) tiles: 0 128x128, 1 256x64, 2 64x256, 3 64x64.
-int auto_cfg(int64_t M, int64_t Ncol) {
+// Pick the tile config (0 128x128, 1 256x64, 2 64x256, 3 64x64) minimising
+//   padded work x per-config efficiency penalty x grid fill,
+// where fill = (launch rounds x resident slots) / tiles charges a grid that leaves CUs idle
+// in its last round (e.g. M=8192 x N=512: 256 tiles of 128x128 fill only half of the 512
+// two-per-CU slots). The small 64x64 tile is only penalised when the GEMM is
+// compute-bound (long K); short-K (memory-bound) GEMMs favour its higher occupancy.
+// Calibrated with tools/conv_bench.py --cfg 0..3 on the ResNet-50 shapes.
+int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim = 0, bool fill = false) {
   const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
-  const double pen[4] = {1.0, 1.04, 1.04, 1.35};
+  const bool long_k = Kdim == 0 || Kdim > 256;
+  const double pen_long[4] = {1.0, 1.04, 1.04, 1.35}, pen_short[4] = {1.0, 1.0, 1.0, 1.05};
+  const double slots[4] = {512, 512, 512, 1280};   // resident blocks chip-wide (LDS/VGPR-limited)
   int best = 0;
   double best_s = 1e300;
   for (int c = 0; c < 4; ++c) {
-    const double padded = (double)((M + bm[c] - 1) / bm[c] * bm[c]) * (double)((Ncol + bn[c] - 1) / bn[c] * bn[c]);
-    const double s = padded * pen[c];
-    if (s < best_s) { best_s = s; best = c; }
+    const int64_t mt = (M + bm[c] - 1) / bm[c], nt = (Ncol + bn[c] - 1) / bn[c];
+    const double padded = (double)(mt * bm[c]) * (double)(nt * bn[c]);
+    double f = 1.0;
+    if (fill) {
+      const double tiles = (double)(mt * nt);
+      f = std::ceil(tiles / slots[c]) * slots[c] / tiles;
+    }
+    const double sc = padded * (long_k ? pen_long[c] : pen_short[c]) * f;
+    if (sc < best_s) { best_s = sc; best = c; }
   }
   return best;
 }
@@ -68,7 +82,7 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
   TORCH_CHECK(g.K % 8 == 0, "Cout must be a multiple of 8");
   c10::DeviceGuard dg(x.device());
   const int64_t M = (int64_t)g.N * g.P * g.Q;
-  if (cfg < 0) cfg = auto_cfg(M, g.K);
+  if (cfg < 0) cfg = auto_cfg(M, g.K, (int64_t)g.R * g.S * g.C, true);
   auto y = torch::empty({g.N, g.P, g.Q, g.K}, x.options());
   torch::Tensor slab;
   float* sp = nullptr;
@@ -100,7 +114,7 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
   TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
   c10::DeviceGuard dg(dy.device());
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = auto_cfg(M, g.C);
+  if (cfg < 0) cfg = auto_cfg(M, g.C, (int64_t)g.R * g.S * g.K / (stride * stride), true);
   torch::Tensor dx;
   if (out.has_value()) {
     dx = *out;
