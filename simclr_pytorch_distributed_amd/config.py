@@ -119,6 +119,9 @@ def pretrain_parser() -> argparse.ArgumentParser:
     g.add_argument("--base_temperature", type=float, default=0.07)
     g.add_argument("--contrast_mode", type=str, default="all", choices=["all", "one"])
     g.add_argument("--resume", type=str, default="", help="resume model+optimizer+epoch+state from a ckpt")
+    g.add_argument("--micro_batch", type=int, default=0,
+                   help="gradient-cache micro-batching: encoder forward/backward in chunks of this many "
+                        "VIEWS per rank (0 = whole local batch); the contrastive loss still sees the full batch")
     _add_common_new_flags(p)
     return p
 

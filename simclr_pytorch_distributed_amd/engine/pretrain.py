@@ -58,6 +58,11 @@ def resolve_backend(requested: str, device: torch.device, stem: str = "cifar") -
     return "native" if native_ok else "torch"
 
 
+def _null():
+    import contextlib
+    return contextlib.nullcontext()
+
+
 def step_seed(base: int, epoch: int, idx: int, rank: int) -> int:
     return (base * 1000003 + epoch * 100003 + idx * 17 + rank * 7919) & ((1 << 62) - 1)
 
@@ -167,6 +172,9 @@ class PretrainEngine:
         """Device work of one step: no host syncs, no host-dependent control flow
         (capturable into a hipGraph)."""
         opt = self.opt
+        mb = getattr(opt, "micro_batch", 0) or 0
+        if 0 < mb < 2 * idx.numel():
+            return self._step_body_gradcache(idx, epoch, it, mb)
         ph = self.prof.phase
         with ph("augment"):
             x = self.make_views(idx, epoch, it)
@@ -180,6 +188,58 @@ class PretrainEngine:
         with ph("backward"):
             self.optimizer.zero_grad()
             loss.backward()
+        if self.reducer is not None:
+            with ph("grad_sync_wait"):
+                self.reducer.finish()
+        with ph("optimizer"):
+            self.optimizer.step()
+        stats["loss_local"] = loss.detach()
+        return stats
+
+    def _step_body_gradcache(self, idx: torch.Tensor, epoch: int, it: int, mb: int):
+        """Gradient-cache step for contrastive batches larger than one encoder pass fits in
+        HBM (e.g. BS 4096 at 224x224, BASELINE config 5): (1) encode all views in chunks of
+        ``mb`` without autograd, (2) contrastive loss + norm terms on the full feature set,
+        backward to the features only, (3) re-encode each chunk with autograd and backprop
+        its slice of the feature gradient. Activation memory is one chunk's; the loss and
+        its gradient are those of the full batch. BatchNorm statistics are per chunk (as
+        in any micro-batched BN network); running statistics are updated once per chunk
+        in the re-encode pass only. The bucket reducer stays paused until the last chunk.
+        """
+        opt = self.opt
+        ph = self.prof.phase
+        with ph("augment"):
+            x = self.make_views(idx, epoch, it)
+            labels = self.labels[idx]
+        chunks = list(torch.split(x, mb))
+        bns = [m for m in self.model.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
+        saved = [(m.running_mean.clone(), m.running_var.clone(), m.num_batches_tracked.clone())
+                 for m in bns if m.running_mean is not None]
+        with ph("forward"), torch.no_grad():
+            feats = torch.cat([self.runner.forward(c) for c in chunks])
+        with torch.no_grad():          # undo the statistics updates of the no-grad pass
+            for m, (rm, rv, nb) in zip([m for m in bns if m.running_mean is not None], saved):
+                m.running_mean.copy_(rm)
+                m.running_var.copy_(rv)
+                m.num_batches_tracked.copy_(nb)
+        feats = feats.detach().requires_grad_(True)
+        with ph("loss"):
+            loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
+            stats = self._norm_terms(feats)
+            loss = loss + stats.pop("extra_loss")
+            loss.backward()
+        gfeat = feats.grad
+        self.optimizer.zero_grad()
+        with ph("backward"):
+            off = 0
+            for i, c in enumerate(chunks):
+                n = c.shape[0]
+                last = i == len(chunks) - 1
+                ctx = self.reducer.no_sync() if (self.reducer is not None and not last) else _null()
+                with ctx:
+                    f = self.runner.forward(c)
+                    f.backward(gfeat[off:off + n].to(f.dtype))
+                off += n
         if self.reducer is not None:
             with ph("grad_sync_wait"):
                 self.reducer.finish()

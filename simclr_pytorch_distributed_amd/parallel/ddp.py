@@ -58,6 +58,7 @@ class GradBucketReducer:
         # sink AND autograd still runs the parameter's AccumulateGrad node (with a None grad),
         # which fires the post-accumulate hook a second time
         self._seen = [False] * len(flat.params)
+        self._paused = False
         self._listener = None
         if self.enabled:
             for i, p in enumerate(flat.params):
@@ -86,7 +87,7 @@ class GradBucketReducer:
     # ---- backward -----------------------------------------------------------------
     def _make_hook(self, i):
         def hook(_p):
-            if self._seen[i]:
+            if self._paused or self._seen[i]:
                 return
             self._seen[i] = True
             b = self.buckets[self.bucket_of[i]]
@@ -108,6 +109,20 @@ class GradBucketReducer:
                 b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
         else:
             b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+
+    def no_sync(self):
+        """Context: gradients produced inside only accumulate locally (no bucket launches),
+        e.g. all but the last micro-batch of a gradient-cache step."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _ctx():
+            prev, self._paused = self._paused, True
+            try:
+                yield
+            finally:
+                self._paused = prev
+        return _ctx()
 
     def finish(self):
         """Wait for all bucket reductions (launching any bucket whose params got no grad)."""

@@ -205,3 +205,30 @@ def _sink_case(rank, world, d):  # noqa: C901
 
 def test_reducer_counts_sink_params_once():
     _run(_sink_case, 2)
+
+
+def _gradcache_case(rank, world, d):
+    """W=2: gradient-cache micro-batching (reducer paused until the last chunk) gives the
+    same update as the whole-batch step (BN in eval mode: batch-independent layers)."""
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    res = []
+    for mb in (0, 4):
+        opt = parse_pretrain(["--model", "resnet18", "--backend", "torch", "--dist_backend", "gloo", "--synthetic",
+                              "--synthetic_size", "64", "--batch_size", str(8 * world), "--ngpu", str(world),
+                              "--micro_batch", str(mb), "--work_dir", os.path.join(d, f"mb{mb}")], make_dirs=False)
+        eng = PretrainEngine(opt)
+        eng.model.load_state_dict(_init_state())
+        eng.model.train()
+        for m in eng.model.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.eval()
+        idx = torch.arange(rank * 8, rank * 8 + 8)
+        eng.train_step(idx, 1, 0, 4)
+        res.append(eng.flat.flat.clone())
+        eng.reducer.remove()
+    assert torch.allclose(res[0], res[1], rtol=1e-4, atol=1e-6)
+
+
+def test_gradcache_two_ranks():
+    _run(_gradcache_case, 2)
