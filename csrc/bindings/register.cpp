@@ -8,6 +8,7 @@ void register_data(pybind11::module& m);
 void register_optim(pybind11::module& m);
 void register_pool(pybind11::module& m);
 void register_wprep(pybind11::module& m);
+void register_xgmi(pybind11::module& m);
 
 void register_ops(pybind11::module& m) {
   register_supcon(m);
@@ -16,5 +17,6 @@ void register_ops(pybind11::module& m) {
   register_optim(m);
   register_pool(m);
   register_wprep(m);
+  register_xgmi(m);
 }
 }  // namespace sdx_bind

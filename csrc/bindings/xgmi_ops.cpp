@@ -1,0 +1,162 @@
+// Bindings for the one-shot xGMI all-reduce (xgmi.hip): IPC arena lifetime, handle
+// exchange (the Python side moves the 64-byte handles over the process group), calls, and
+// the single-GPU W-rank emulation used by the tests.
+#include "ops_decl.h"
+#include "launchers.h"
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace sdx_bind {
+namespace {
+
+struct Arena {
+  int device = 0;
+  int rank = 0;
+  int world = 1;
+  size_t cap = 0;
+  void* base = nullptr;            // own arena: data then flags
+  std::vector<void*> opened;       // peer arenas mapped through IPC
+  XgmiPeers peers{};
+  unsigned epoch = 0;
+  torch::Tensor err;               // device int32 error word (sender index + 1)
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Arena>> g_arenas;
+
+size_t arena_bytes(int world, size_t cap) {
+  const size_t data = 2ull * world * cap * sizeof(double);
+  return data + 256;   // flags [2][W] u32 (≤ 64 B) after the data, 256-B aligned block
+}
+
+Arena& get(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(id >= 0 && id < (int64_t)g_arenas.size() && g_arenas[id], "bad xgmi arena id");
+  return *g_arenas[id];
+}
+
+void set_ptrs(XgmiPeers& p, int q, void* base, int world, size_t cap) {
+  p.data[q] = static_cast<double*>(base);
+  p.flags[q] = reinterpret_cast<unsigned*>(static_cast<char*>(base) + 2ull * world * cap * sizeof(double));
+}
+
+int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap) {
+  TORCH_CHECK(world >= 1 && world <= kXgmiMaxPeers && rank >= 0 && rank < world, "1 <= world <= 8");
+  TORCH_CHECK(cap > 0 && cap <= (1 << 20), "cap in (0, 2^20]");
+  auto a = std::make_unique<Arena>();
+  check_hip(hipGetDevice(&a->device), "hipGetDevice");
+  a->rank = (int)rank;
+  a->world = (int)world;
+  a->cap = (size_t)cap;
+  const size_t bytes = arena_bytes(a->world, a->cap);
+  // uncached: peers' remote stores must be seen by this GPU's loads without cache maintenance
+  check_hip(hipExtMallocWithFlags(&a->base, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  check_hip(hipMemset(a->base, 0, bytes), "hipMemset");
+  a->peers.cap = a->cap;
+  set_ptrs(a->peers, a->rank, a->base, a->world, a->cap);
+  a->err = torch::zeros({1}, torch::TensorOptions().dtype(at::kInt).device(torch::kCUDA, a->device));
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_arenas.push_back(std::move(a));
+  return (int64_t)g_arenas.size() - 1;
+}
+
+torch::Tensor xgmi_handle(int64_t id) {
+  Arena& a = get(id);
+  hipIpcMemHandle_t h;
+  check_hip(hipIpcGetMemHandle(&h, a.base), "hipIpcGetMemHandle");
+  auto t = torch::empty({HIP_IPC_HANDLE_SIZE}, torch::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr<uint8_t>(), &h, HIP_IPC_HANDLE_SIZE);
+  return t;
+}
+
+void xgmi_open(int64_t id, torch::Tensor handles) {
+  Arena& a = get(id);
+  TORCH_CHECK(handles.dtype() == at::kByte && handles.dim() == 2 && handles.size(0) == a.world &&
+                  handles.size(1) == HIP_IPC_HANDLE_SIZE && !handles.is_cuda(),
+              "handles: CPU uint8 [world, 64]");
+  auto hc = handles.contiguous();
+  for (int q = 0; q < a.world; ++q) {
+    if (q == a.rank) continue;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, hc.data_ptr<uint8_t>() + (size_t)q * HIP_IPC_HANDLE_SIZE, HIP_IPC_HANDLE_SIZE);
+    void* p = nullptr;
+    check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    a.opened.push_back(p);
+    set_ptrs(a.peers, q, p, a.world, a.cap);
+  }
+}
+
+torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x) {
+  Arena& a = get(id);
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.is_contiguous(), "x: contiguous fp64 GPU tensor");
+  TORCH_CHECK((size_t)x.numel() <= a.cap, "message larger than the arena slot");
+  c10::DeviceGuard dg(x.device());
+  auto out = torch::empty_like(x);
+  a.epoch += 1;
+  check_hip(launch_xgmi_allreduce(x.data_ptr<double>(), out.data_ptr<double>(), (int)x.numel(), a.peers, a.rank,
+                                  a.world, a.epoch, a.err.data_ptr<int>(), cur_stream()),
+            "xgmi_allreduce");
+  return out;
+}
+
+int64_t xgmi_error(int64_t id) {
+  Arena& a = get(id);
+  return a.err.cpu().item<int>();
+}
+
+void xgmi_destroy(int64_t id) {
+  std::unique_ptr<Arena> a;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    TORCH_CHECK(id >= 0 && id < (int64_t)g_arenas.size() && g_arenas[id], "bad xgmi arena id");
+    a = std::move(g_arenas[id]);
+  }
+  (void)hipDeviceSynchronize();
+  for (void* p : a->opened) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(a->base);
+}
+
+// W virtual ranks on this GPU: `in` [W, n] fp64; runs `iters` calls (epochs 1..iters, so both
+// parities and arena reuse are exercised) and returns the last result [W, n].
+torch::Tensor xgmi_emulate(torch::Tensor in, int64_t iters) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kDouble && in.dim() == 2 && in.is_contiguous(),
+              "in: [W, n] fp64 GPU");
+  const int world = (int)in.size(0);
+  const int n = (int)in.size(1);
+  TORCH_CHECK(world >= 1 && world <= kXgmiMaxPeers && iters >= 1, "1 <= W <= 8");
+  c10::DeviceGuard dg(in.device());
+  const size_t cap = (size_t)std::max(n, 1);
+  auto opts = in.options().dtype(at::kByte);
+  std::vector<torch::Tensor> arenas;
+  XgmiPeers peers{};
+  peers.cap = cap;
+  for (int q = 0; q < world; ++q) {
+    arenas.push_back(torch::zeros({(int64_t)arena_bytes(world, cap)}, opts));
+    set_ptrs(peers, q, arenas.back().data_ptr(), world, cap);
+  }
+  auto out = torch::empty_like(in);
+  auto err = torch::zeros({1}, in.options().dtype(at::kInt));
+  for (int64_t e = 1; e <= iters; ++e)
+    check_hip(launch_xgmi_emulate(in.data_ptr<double>(), out.data_ptr<double>(), n, peers, world, (unsigned)e,
+                                  err.data_ptr<int>(), cur_stream()),
+              "xgmi_emulate");
+  const int ev = err.cpu().item<int>();
+  TORCH_CHECK(ev == 0, "xgmi emulation: flag wait timed out (sender ", ev - 1, ")");
+  return out;
+}
+
+}  // namespace
+
+void register_xgmi(pybind11::module& m) {
+  m.def("xgmi_create", &xgmi_create, "allocate this rank's IPC receive arena (uncached device memory)");
+  m.def("xgmi_handle", &xgmi_handle, "64-byte IPC handle of this rank's arena");
+  m.def("xgmi_open", &xgmi_open, "map every peer's arena from their IPC handles [W, 64]");
+  m.def("xgmi_allreduce", &xgmi_allreduce, "one-shot fp64 all-reduce (sum) of a small tensor");
+  m.def("xgmi_error", &xgmi_error, "nonzero: a peer's flag never arrived (1 + sender)");
+  m.def("xgmi_destroy", &xgmi_destroy);
+  m.def("xgmi_emulate", &xgmi_emulate, "single-GPU W-rank emulation of the one-shot protocol");
+}
+
+}  // namespace sdx_bind

@@ -113,3 +113,15 @@ hipError_t launch_gap_bwd(const float* dy, void* dx, int N, int HW, int C, hipSt
 // ---- weight preparation (wprep.hip) ---------------------------------------------
 // segs: device table of nseg rows {src, dst_k, dst_t, K|RS<<32, C|Cp<<32, n, start} (int64)
 hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s);
+
+// ---- one-shot small all-reduce over xGMI peer memory (xgmi.hip) --------------------
+constexpr int kXgmiMaxPeers = 8;
+struct XgmiPeers {
+  double* data[kXgmiMaxPeers];     // each rank's receive arena: [2][W][cap] fp64 (IPC-mapped)
+  unsigned* flags[kXgmiMaxPeers];  // each rank's flags: [2][W] u32
+  size_t cap;                      // elements per slot
+};
+hipError_t launch_xgmi_allreduce(const double* in, double* out, int n, const XgmiPeers& peers, int me, int world,
+                                 unsigned epoch, int* err, hipStream_t s);
+hipError_t launch_xgmi_emulate(const double* in, double* out, int n, const XgmiPeers& peers, int world,
+                               unsigned epoch, int* err, hipStream_t s);

@@ -68,6 +68,8 @@ def _add_common_new_flags(p: argparse.ArgumentParser):
     g.add_argument("--cuda_graph", action="store_true", help="capture the train step in a HIP graph")
     g.add_argument("--max_steps", type=int, default=0, help="stop each epoch after this many steps (0 = all)")
     g.add_argument("--gpu_aug", type=int, default=1, help="run augmentation on the GPU (1) or CPU (0)")
+    g.add_argument("--syncbn_comm", type=str, default="rccl", choices=["rccl", "xgmi"],
+                   help="SyncBN statistic all-reduce: RCCL, or the one-shot xGMI peer-memory kernel")
     g.add_argument("--comm_timeout", type=float, default=600.0,
                    help="collective timeout in seconds (a dead/stalled peer raises instead of hanging)")
     g.add_argument("--profile", action="store_true",

@@ -94,6 +94,13 @@ class PretrainEngine:
                 model = convert_sync_bn(model)
             else:
                 self.sync_group = dist.group.WORLD
+                if getattr(opt, "syncbn_comm", "rccl") == "xgmi":
+                    try:
+                        from ..parallel.xgmi import OneShotAllReduce
+                        comm.set_small_allreduce(None, OneShotAllReduce())
+                        logging.info("SyncBN statistics: one-shot xGMI all-reduce")
+                    except Exception as e:  # noqa: BLE001
+                        logging.warning(f"one-shot xGMI all-reduce unavailable ({e}); using RCCL")
         model = model.to(dev)
         if dev.type == "cuda":
             model = model.to(memory_format=torch.channels_last)

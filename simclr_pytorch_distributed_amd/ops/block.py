@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from . import _ext, sinks
+from ..parallel import comm
 from .streams import SideWork
 
 
@@ -52,7 +53,7 @@ class _BN:
             if group is None:
                 return tuple(m.bn_stats_finalize(slab, *args))
             sums = m.bn_stats_reduce(slab)
-            dist.all_reduce(sums, group=group)
+            comm.small_all_reduce_(sums, group)
             sc, sh, mean, inv = m.bn_finalize(sums, *args)
             return sc, sh, mean, inv
         sc, sh = m.bn_eval_affine(bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.eps)
@@ -89,7 +90,7 @@ def _bn_bwd(m, dout, out, y, mean, inv, bn, count, group, y_b=None, mean_b=None,
                                                   bn.weight.detach(), inv, gb, inv_b, **snk)
     else:
         s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b, msc, msh)
-        dist.all_reduce(s, group=group)
+        comm.small_all_reduce_(s, group)
         ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, gb, mean_b, inv_b, **snk)
     if y_b is None:
         dya, _, dz = m.bn_bwd_apply(dout, out, y, ca, None, None, want_dz, msc, msh)

@@ -121,6 +121,30 @@ def all_gather_with_grad(x: torch.Tensor) -> torch.Tensor:
     return _AllGatherGrad.apply(x)
 
 
+_small = {}
+
+
+def set_small_allreduce(group, impl) -> None:
+    """Route :func:`small_all_reduce_` for ``group`` (None = WORLD) through ``impl``
+    (e.g. :class:`parallel.xgmi.OneShotAllReduce`); ``impl=None`` restores RCCL/gloo."""
+    key = id(group) if group is not None else None
+    if impl is None:
+        _small.pop(key, None)
+    else:
+        _small[key] = impl
+
+
+def small_all_reduce_(x: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place sum of a small, latency-bound tensor (SyncBN statistics)."""
+    impl = _small.get(id(group) if group is not None else None)
+    if impl is None and group is dist.group.WORLD:
+        impl = _small.get(None)
+    if impl is not None and x.is_cuda and x.dtype == torch.float64:
+        return impl.all_reduce_(x)
+    dist.all_reduce(x, group=group)
+    return x
+
+
 def all_reduce_sum_(x: torch.Tensor) -> torch.Tensor:
     if world_size() > 1:
         dist.all_reduce(x)
