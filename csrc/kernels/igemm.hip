@@ -71,11 +71,13 @@ __device__ __forceinline__ int kin_off(int row, int ch) {
 // K-outer image: [BK][COLS] bf16; chunk swizzle keeps the transposed reads of a 32-lane
 // half (8 rows x 2 chunks) on distinct banks.
 template <int COLS>
+__device__ __forceinline__ int kout_swz(int row) {
+  if (COLS >= 128) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;
+}
+template <int COLS>
 __device__ __forceinline__ int kout_off(int row, int ch) {
-  int sw;
-  if (COLS >= 128) sw = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-  else sw = (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;
-  return row * (COLS * 2) + ((ch ^ sw) << 4);
+  return row * (COLS * 2) + ((ch ^ kout_swz<COLS>(row)) << 4);
 }
 
 __device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
@@ -155,7 +157,6 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   // tid/8 + 32*i. LDS-DMA: instruction i of wave w fills rows 8*(w*CH + i) .. +7 (1 KiB),
   // lane L row +L/8 at physical chunk L%8, i.e. logical chunk (L&7)^(L>>3).
   constexpr bool GL = DEPTH == 3;
-  static_assert(!GL || MODE != MODE_WGRAD, "LDS-DMA staging covers the K-inner operands");
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
   const int kin_ch = GL ? ((lane & 7) ^ ((lane >> 3) & 7)) : (tid & 7);
   const int kin_row0 = tid >> 3;
@@ -218,6 +219,28 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     const int rs = jj / g.C;
     wb_r = rs / g.S;
     wb_s = rs - wb_r * g.S;
+  }
+  // WGRAD with LDS-DMA: instruction i of wave w fills bytes [1 KiB x (w*CH + i), +1 KiB) of
+  // the K-outer image; lane L lands at byte 16L of it = (row, physical chunk), which holds
+  // logical chunk phys ^ swizzle(row). B columns (r, s, c) are decoded once per instruction.
+  constexpr int GB_CH = (MODE == MODE_WGRAD && GL) ? T::B_CH : 1;
+  int gb_row[GB_CH], gb_r[GB_CH], gb_s[GB_CH], gb_c[GB_CH];
+  bool gb_ok[GB_CH];
+  if (MODE == MODE_WGRAD && GL) {
+#pragma unroll
+    for (int i = 0; i < GB_CH; ++i) {
+      const int byte = (wvu * T::B_CH + i) * 1024 + lane * 16;
+      const int row = byte / (BN * 2), phys = (byte % (BN * 2)) >> 4;
+      const int ch = phys ^ kout_swz<BN>(row);
+      const int j0 = n0 + ch * 8;
+      gb_row[i] = row;
+      gb_ok[i] = j0 < p.Ncol;
+      const int jj = gb_ok[i] ? j0 : 0;
+      gb_c[i] = jj % g.C;
+      const int rs = jj / g.C;
+      gb_r[i] = rs / g.S;
+      gb_s[i] = rs - gb_r[i] * g.S;
+    }
   }
   // WGRAD: fused BN+ReLU of the activation operand (channel chunk fixed per thread)
   const bool wb_bn = (MODE == MODE_WGRAD) && p.in_scale != nullptr;
@@ -324,6 +347,44 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   auto issue_glds = [&](int k0, int buf) {
     unsigned char* sa = smem + buf * T::STAGE;
     unsigned char* sb = sa + T::A_BYTES;
+    if (MODE == MODE_WGRAD) {
+      // A: dy [pixels][K] rows of the tile, BM couts each
+#pragma unroll
+      for (int i = 0; i < T::A_CH; ++i) {
+        const int byte = (wvu * T::A_CH + i) * 1024 + lane * 16;
+        const int row = byte / (BM * 2), phys = (byte % (BM * 2)) >> 4;
+        const int ch = phys ^ kout_swz<BM>(row);
+        const int kk = k0 + row, co = m0 + ch * 8;
+        const bool ok = kk < k_end && co < p.M;
+        const uint16_t* src = ok ? p.a + kk * g.K + co : g_zero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(sa + (wvu * T::A_CH + i) * 1024),
+                                         16, 0, 0);
+      }
+      // B: im2col(x) rows (pixels) x BN (r, s, c) columns
+#pragma unroll
+      for (int i = 0; i < GB_CH; ++i) {
+        const int kk = k0 + gb_row[i];
+        bool ok = gb_ok[i] && kk < k_end;
+        int off;
+        if (is1x1) {
+          off = kk * g.C + gb_c[i];
+        } else {
+          const int n = (int)fdiv((unsigned)kk, p.div_pq);
+          const int rem = kk - n * g.P * g.Q;
+          const int pp = (int)fdiv((unsigned)rem, p.div_q);
+          const int qq = rem - pp * g.Q;
+          const int yy = pp * g.stride - g.pad + gb_r[i], xx = qq * g.stride - g.pad + gb_s[i];
+          ok = ok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
+          off = ((n * g.H + yy) * g.W + xx) * g.C + gb_c[i];
+        }
+        const uint16_t* src = ok ? p.b + off : g_zero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(sb + (wvu * T::B_CH + i) * 1024),
+                                         16, 0, 0);
+      }
+      return;
+    }
     const int k = k0 + kin_ch * 8;
     const bool kok = k < k_end;
 #pragma unroll
@@ -674,11 +735,11 @@ int igemm_depth() {
   return d;
 }
 
-// LDS-DMA operand staging for FWD/DGRAD (SDX_IGEMM_GLDS=0 disables)
+// LDS-DMA operand staging: 0 off, 1 FWD/DGRAD (default), 2 FWD/DGRAD/WGRAD
 int igemm_glds() {
   static const int a = [] {
     const char* e = getenv("SDX_IGEMM_GLDS");
-    return (e && e[0] == '0') ? 0 : 1;
+    return e ? atoi(e) : 1;
   }();
   return a;
 }
@@ -700,8 +761,10 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   // depth 2 only where the second register stage fits without spilling (checked with
   // -Rpass-analysis=kernel-resource-usage)
   constexpr bool kDepth2 = (BM == 64 && BN == 64) || (MODE == MODE_FWD && BM != 256);
-  if constexpr (MODE != MODE_WGRAD) {
-    if (p.in_scale == nullptr && igemm_glds()) {
+  {
+    // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
+    // (SDX_IGEMM_GLDS=2 enables it there too)
+    if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
       hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 3>), dim3(grid), dim3(256), 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;

@@ -9,11 +9,12 @@ math: networks/resnet_big.py:7-67), which lets the executor
 * fuse the residual-gradient sum into the last data-gradient GEMM epilogue
   (``dx = dgrad(conv1) + dgrad(shortcut) | + dz``) instead of a separate add pass;
 * run SyncBN as one fp64 all-reduce per BN per direction;
-* never materialise the block-internal activations ``relu(bn1(y1))`` / ``relu(bn2(y2))``:
-  the consuming conv applies BN+ReLU in its operand-load prologue (forward and weight
-  gradient), and the BN backward recomputes the ReLU mask from ``y`` — saving one
-  write + two reads of every internal activation per step (``SDX_FUSE_PROLOGUE=0``
-  restores the materialised path).
+* optionally (``SDX_FUSE_PROLOGUE=1``) never materialise the block-internal activations
+  ``relu(bn1(y1))`` / ``relu(bn2(y2))``: the consuming conv applies BN+ReLU in its
+  operand-load prologue (forward and weight gradient) and the BN backward recomputes the
+  ReLU mask from ``y``. That saves one write + two reads per internal activation but
+  forces register staging on those convs; with LDS-DMA staged convs the materialised
+  path is faster, so it is the default.
 
 Parameters are passed to ``apply`` only to keep the autograd graph connected (their
 returned gradients are ``None``: the sinks already hold them); the bucket reducer is
@@ -32,7 +33,9 @@ from ..parallel import comm
 from .streams import SideWork
 
 
-FUSE_PROLOGUE = os.environ.get("SDX_FUSE_PROLOGUE", "1") != "0"
+# off by default: with LDS-DMA staged convs, materialising relu(bn(y)) once is faster than
+# the register-staged prologue conv (16.9 vs 17.3 ms/step, ResNet-50 bench)
+FUSE_PROLOGUE = os.environ.get("SDX_FUSE_PROLOGUE", "0") == "1"
 
 
 def _world(group) -> int:
