@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""From a rocprofv3 kernel trace of bench.py: wall time of the last training step
+(sgd_kernel end to sgd_kernel end), GPU-busy time (union of kernel intervals over all
+streams) and idle gaps, plus the busiest kernels of that step.
+
+python tools/step_timeline.py <rocprof dir>
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    d = sys.argv[1]
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    rows = list(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+    a, b = idx[-2], idx[-1]
+    t0, t1 = int(rows[a]["End_Timestamp"]), int(rows[b]["End_Timestamp"])
+    busy, cur, gaps = 0, t0, []
+    per = defaultdict(float)
+    for r in rows[a + 1:b + 1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        per[r["Kernel_Name"].split("(")[0][:80]] += (e - s) / 1e3
+        if s > cur:
+            gaps.append((s - cur) / 1e3)
+        if e <= cur:
+            continue
+        busy += e - max(s, cur)
+        cur = e
+    print(f"last step: wall {(t1 - t0) / 1e3:.1f} us, GPU busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us "
+          f"in {len(gaps)} gaps (largest {max(gaps) if gaps else 0:.1f} us), kernels {b - a}")
+    for k, v in sorted(per.items(), key=lambda kv: -kv[1])[:12]:
+        print(f"  {v:8.1f} us  {k}")
+
+
+if __name__ == "__main__":
+    main()
