@@ -164,10 +164,11 @@ class _Bottleneck(torch.autograd.Function):
             dy3, _, dz = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group, want_dz=True)
         _wgrad(m, dy3, y2 if f2 else a2, blk.conv3, 1, 0, f2)
         da2 = m.conv_dgrad(dy3, wc.dgrad(blk.conv3), y2.shape[1], y2.shape[2], 1, 0)
-        dy2, _, _ = _bn_bwd(m, da2, a2, y2, mu2, iv2, blk.bn2, cnt2, group, mask=f2)
+        # ReLU mask recomputed from y (read anyway) instead of reading the activation
+        dy2, _, _ = _bn_bwd(m, da2, None, y2, mu2, iv2, blk.bn2, cnt2, group, mask=(sc2, sh2))
         _wgrad(m, dy2, y1 if f1 else a1, blk.conv2, st, 1, f1)
         da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), H, W, st, 1)
-        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt1, group, mask=f1)
+        dy1, _, _ = _bn_bwd(m, da1, None, y1, mu1, iv1, blk.bn1, cnt1, group, mask=(sc1, sh1))
         _wgrad(m, dy1, x, blk.conv1, 1, 0)
         if proj:
             _wgrad(m, dys, x, blk.shortcut[0], st, 0)
@@ -221,7 +222,7 @@ class _Basic(torch.autograd.Function):
             dy2, _, dz = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group, want_dz=True)
         _wgrad(m, dy2, y1 if f1 else a1, blk.conv2, 1, 1, f1)
         da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), y1.shape[1], y1.shape[2], 1, 1)
-        dy1, _, _ = _bn_bwd(m, da1, a1, y1, mu1, iv1, blk.bn1, cnt, group, mask=f1)
+        dy1, _, _ = _bn_bwd(m, da1, None, y1, mu1, iv1, blk.bn1, cnt, group, mask=(sc1, sh1))
         _wgrad(m, dy1, x, blk.conv1, st, 1)
         if proj:
             _wgrad(m, dys, x, blk.shortcut[0], st, 0)
@@ -247,18 +248,18 @@ class _Stem(torch.autograd.Function):
         a = m.bn_apply(y, sc, sh, None, None, None, 0, True)
         out = m.maxpool_fwd(a, 3, 2, 1) if imagenet else a
         if training:
-            ctx.save_for_backward(x, y, a, out, mu, iv)
+            ctx.save_for_backward(x, y, a if imagenet else None, out if imagenet else None, mu, iv, sc, sh)
             ctx.enc, ctx.group, ctx.params, ctx.cnt, ctx.geo = enc, group, params, cnt, (st, pad, imagenet)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         m = _ext.require()
-        x, y, a, out, mu, iv = ctx.saved_tensors
+        x, y, a, out, mu, iv, sc, sh = ctx.saved_tensors
         st, pad, imagenet = ctx.geo
         dout = dout.contiguous()
         da = m.maxpool_bwd(a, out, dout, 3, 2, 1) if imagenet else dout
-        dy, _, _ = _bn_bwd(m, da, a, y, mu, iv, ctx.enc.bn1, ctx.cnt, ctx.group)
+        dy, _, _ = _bn_bwd(m, da, None, y, mu, iv, ctx.enc.bn1, ctx.cnt, ctx.group, mask=(sc, sh))
         w = ctx.enc.conv1.weight
         K, C, R, S = w.shape
         g = sinks.target(w)
