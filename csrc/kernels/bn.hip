@@ -201,48 +201,64 @@ __global__ void bn_eval_affine_kernel(int C, const float* __restrict__ gamma, co
   shift[c] = (beta ? beta[c] : 0.f) - rm[c] * g * invstd;
 }
 
+__device__ __forceinline__ void load8c(const float* __restrict__ p, float (&v)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // out = act(y*sc + sh [+ r*sc2 + sh2 | + r])     res_mode: 0 none, 1 bn'd residual, 2 raw residual
+// 32-bit indexing (tensors < 2^31 elements). When the grid stride is a multiple of C/8
+// (always for power-of-two C <= 2048) the channel group is fixed per thread: the per-channel
+// coefficients are loaded once into registers.
 template <int RES, bool RELU>
-__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ sc,
-                                                       const float* __restrict__ sh, const uint16_t* __restrict__ r,
-                                                       const float* __restrict__ sc2, const float* __restrict__ sh2,
-                                                       uint16_t* __restrict__ out, long n8l, int C8) {
-  // 32-bit indexing (tensors < 2^31 elements); the channel group stays fixed per thread
-  // whenever the grid stride is a multiple of C/8 (no per-element modulo)
-  const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
-  const bool fixed = (stride % C8) == 0;
-  const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
-  int c0 = (e0 % C8) * 8;
-  for (int e = e0; e < n8; e += stride) {
-    if (!fixed) c0 = (e % C8) * 8;
+struct ApplyOp {
+  float ss[8], tt[8], aa[8], bb[8];
+  __device__ __forceinline__ void load(const float* sc, const float* sh, const float* sc2, const float* sh2, int c0) {
+    load8c(sc + c0, ss);
+    load8c(sh + c0, tt);
+    if (RES == 1) {
+      load8c(sc2 + c0, aa);
+      load8c(sh2 + c0, bb);
+    }
+  }
+  __device__ __forceinline__ uint4 run(uint4 yv, uint4 rv4) const {
     float v[8];
-    unpack8(reinterpret_cast<const uint4*>(y)[e], v);
-    const float4 s0 = reinterpret_cast<const float4*>(sc + c0)[0], s1 = reinterpret_cast<const float4*>(sc + c0)[1];
-    const float4 t0 = reinterpret_cast<const float4*>(sh + c0)[0], t1 = reinterpret_cast<const float4*>(sh + c0)[1];
-    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float tt[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    unpack8(yv, v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = v[i] * ss[i] + tt[i];
     if (RES != 0) {
       float rv[8];
-      unpack8(reinterpret_cast<const uint4*>(r)[e], rv);
-      if (RES == 1) {
-        const float4 a0 = reinterpret_cast<const float4*>(sc2 + c0)[0], a1 = reinterpret_cast<const float4*>(sc2 + c0)[1];
-        const float4 b0 = reinterpret_cast<const float4*>(sh2 + c0)[0], b1 = reinterpret_cast<const float4*>(sh2 + c0)[1];
-        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      unpack8(rv4, rv);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += rv[i] * aa[i] + bb[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += rv[i];
-      }
+      for (int i = 0; i < 8; ++i) v[i] += RES == 1 ? rv[i] * aa[i] + bb[i] : rv[i];
     }
     if (RELU) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.f);
     }
-    reinterpret_cast<uint4*>(out)[e] = pack8(v);
+    return pack8(v);
+  }
+};
+
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ sc,
+                                                       const float* __restrict__ sh, const uint16_t* __restrict__ r,
+                                                       const float* __restrict__ sc2, const float* __restrict__ sh2,
+                                                       uint16_t* __restrict__ out, long n8l, int C8) {
+  const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
+  const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint4* Y = reinterpret_cast<const uint4*>(y);
+  const uint4* R = reinterpret_cast<const uint4*>(r);
+  uint4* O = reinterpret_cast<uint4*>(out);
+  ApplyOp<RES, RELU> op;
+  if ((stride % C8) == 0) {
+    op.load(sc, sh, sc2, sh2, (e0 % C8) * 8);
+    for (int e = e0; e < n8; e += stride) O[e] = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+  } else {
+    for (int e = e0; e < n8; e += stride) {
+      op.load(sc, sh, sc2, sh2, (e % C8) * 8);
+      O[e] = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+    }
   }
 }
 
@@ -278,13 +294,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     mkt[i] = mask_y ? msh[c0 + i] : 0.f;
   }
   float s0[8] = {0}, s1[8] = {0}, s2[8] = {0};
-  for (long e = tid; e < n8; e += stride) {
+  const uint4* D = reinterpret_cast<const uint4*>(dout);
+  const uint4* OV = reinterpret_cast<const uint4*>(outv);
+  const uint4* YA = reinterpret_cast<const uint4*>(ya);
+  const uint4* YB = reinterpret_cast<const uint4*>(yb);
+  auto accum = [&](uint4 dv, uint4 ov, uint4 av, uint4 bv) {
     float d[8], a[8];
-    unpack8(reinterpret_cast<const uint4*>(dout)[e], d);
-    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
+    unpack8(dv, d);
+    unpack8(av, a);
     if (outv) {
       float o[8];
-      unpack8(reinterpret_cast<const uint4*>(outv)[e], o);
+      unpack8(ov, o);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
     } else if (mask_y) {
@@ -298,11 +318,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     }
     if (TWO) {
       float b[8];
-      unpack8(reinterpret_cast<const uint4*>(yb)[e], b);
+      unpack8(bv, b);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s2[i] += d[i] * (b[i] - mub[i]);
     }
-  }
+  };
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  // (a 2-chunk unrolled trip measured slower on the 256-channel layer-1 tensors)
+  for (long e = tid; e < n8; e += stride) accum(D[e], outv ? OV[e] : z, YA[e], TWO ? YB[e] : z);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     red[0][threadIdx.x][i] = s0[i];
@@ -339,6 +362,53 @@ __global__ void bn_bwd_coef_kernel(const double* __restrict__ sums, int nsets, i
 }
 
 template <bool TWO>
+struct BwdApplyOp {
+  float A[8], Dc[8], E[8], B2[8], D2[8], E2[8], ms[8], mt[8];
+  bool use_mask;
+  __device__ __forceinline__ void load(const float* ca, const float* cb, const float* msc, const float* msh, int C,
+                                       int c0) {
+    load8c(ca + c0, A);
+    load8c(ca + C + c0, Dc);
+    load8c(ca + 2 * C + c0, E);
+    if (TWO) {
+      load8c(cb + c0, B2);
+      load8c(cb + C + c0, D2);
+      load8c(cb + 2 * C + c0, E2);
+    }
+    use_mask = msc != nullptr;
+    if (use_mask) {
+      load8c(msc + c0, ms);
+      load8c(msh + c0, mt);
+    }
+  }
+  // returns dz (masked dout) in d, writes dya / dyb values
+  __device__ __forceinline__ void run(uint4 dv, uint4 ov, bool has_out, uint4 av, uint4 bv, float (&d)[8],
+                                      uint4& ra, uint4& rb) const {
+    float a[8], r[8];
+    unpack8(dv, d);
+    unpack8(av, a);
+    if (has_out) {
+      float o[8];
+      unpack8(ov, o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
+    } else if (use_mask) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = a[i] * ms[i] + mt[i] > 0.f ? d[i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = A[i] * d[i] + Dc[i] * a[i] + E[i];
+    ra = pack8(r);
+    if (TWO) {
+      unpack8(bv, a);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = B2[i] * d[i] + D2[i] * a[i] + E2[i];
+      rb = pack8(r);
+    }
+  }
+};
+
+template <bool TWO>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout,
                                                            const uint16_t* __restrict__ outv,
                                                            const uint16_t* __restrict__ ya, const float* __restrict__ ca,
@@ -348,32 +418,32 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            const float* __restrict__ msc,
                                                            const float* __restrict__ msh) {
   const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
-  const bool fixed = (stride % C8) == 0;
   const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
-  int c0 = (e0 % C8) * 8;
-  for (int e = e0; e < n8; e += stride) {
-    if (!fixed) c0 = (e % C8) * 8;
-    float d[8], a[8], r[8];
-    unpack8(reinterpret_cast<const uint4*>(dout)[e], d);
-    unpack8(reinterpret_cast<const uint4*>(ya)[e], a);
-    if (outv) {
-      float o[8];
-      unpack8(reinterpret_cast<const uint4*>(outv)[e], o);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = o[i] > 0.f ? d[i] : 0.f;
-    } else if (msc) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = a[i] * msc[c0 + i] + msh[c0 + i] > 0.f ? d[i] : 0.f;
-    }
-    if (dz_out) reinterpret_cast<uint4*>(dz_out)[e] = pack8(d);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = ca[c0 + i] * d[i] + ca[C + c0 + i] * a[i] + ca[2 * C + c0 + i];
-    reinterpret_cast<uint4*>(dya)[e] = pack8(r);
-    if (TWO) {
-      unpack8(reinterpret_cast<const uint4*>(yb)[e], a);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) r[i] = cb[c0 + i] * d[i] + cb[C + c0 + i] * a[i] + cb[2 * C + c0 + i];
-      reinterpret_cast<uint4*>(dyb)[e] = pack8(r);
+  const uint4* D = reinterpret_cast<const uint4*>(dout);
+  const uint4* OV = reinterpret_cast<const uint4*>(outv);
+  const uint4* YA = reinterpret_cast<const uint4*>(ya);
+  const uint4* YB = reinterpret_cast<const uint4*>(yb);
+  uint4* DA = reinterpret_cast<uint4*>(dya);
+  uint4* DB = reinterpret_cast<uint4*>(dyb);
+  uint4* DZ = reinterpret_cast<uint4*>(dz_out);
+  const bool has_out = outv != nullptr;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  BwdApplyOp<TWO> op;
+  auto one = [&](int e, uint4 dv, uint4 ov, uint4 av, uint4 bv) {
+    float d[8];
+    uint4 ra, rb;
+    op.run(dv, ov, has_out, av, bv, d, ra, rb);
+    if (DZ) DZ[e] = pack8(d);
+    DA[e] = ra;
+    if (TWO) DB[e] = rb;
+  };
+  if ((stride % C8) == 0) {
+    op.load(ca, cb, msc, msh, C, (e0 % C8) * 8);
+    for (int e = e0; e < n8; e += stride) one(e, D[e], has_out ? OV[e] : z, YA[e], TWO ? YB[e] : z);
+  } else {
+    for (int e = e0; e < n8; e += stride) {
+      op.load(ca, cb, msc, msh, C, (e % C8) * 8);
+      one(e, D[e], has_out ? OV[e] : z, YA[e], TWO ? YB[e] : z);
     }
   }
 }
