@@ -92,11 +92,22 @@ def main():
     for i in range(a.warmup):
         eng.train_step(next_idx(i), 1, i % iters, iters)
     sync()
+    # host cost of issuing one step into an idle queue (diagnostic, stderr)
+    th = []
+    for i in range(3):
+        sync()
+        t = time.perf_counter()
+        eng.train_step(next_idx(i), 1, i % iters, iters)
+        th.append(time.perf_counter() - t)
+        sync()
+    print(f"host issue time (idle queue) {min(th) * 1e3:.3f} ms/step", file=sys.stderr)
     t0 = time.perf_counter()
     for i in range(a.steps):
         st = eng.train_step(next_idx(i), 1, i % iters, iters)
+    t_host = time.perf_counter() - t0      # host issue time (no sync inside the loop)
     sync()
     dt = time.perf_counter() - t0
+    print(f"host issue time {t_host / a.steps * 1e3:.3f} ms/step", file=sys.stderr)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -3,6 +3,10 @@
 #include "ops_decl.h"
 #include "launchers.h"
 
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -536,6 +540,192 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
   return {dya, dyb, dz};
 }
 
+
+// =====================================================================================
+// Native residual-block executor: the whole forward / backward kernel sequence of a
+// Bottleneck or BasicBlock (reference math: networks/resnet_big.py:7-67) in ONE host
+// call, so the per-kernel Python + binding overhead (≈15-25 µs per launch, measured)
+// leaves the training step. Single-process BN statistics only (SyncBN keeps the Python
+// path, which interleaves the cross-rank all-reduces). Weight gradients run on the caller's
+// side stream (fork/join by events, tensors recorded on that stream for the allocator).
+// =====================================================================================
+
+struct BnState {          // per-BN forward results kept for backward
+  torch::Tensor sc, sh, mu, iv;
+};
+
+BnState bn_forward(const torch::Tensor& slab, double count, const torch::Tensor& g, const torch::Tensor& b,
+                   const torch::Tensor& rm, const torch::Tensor& rv, double eps, double mom, bool training) {
+  if (training) {
+    auto r = bn_stats_finalize(slab, count, g, b, eps, mom, true, rm, rv);
+    return {r[0], r[1], r[2], r[3]};
+  }
+  auto r = bn_eval_affine(g, b, rm, rv, eps);
+  return {r[0], r[1], torch::Tensor(), torch::Tensor()};
+}
+
+double rows_of(const torch::Tensor& y) { return (double)(y.numel() / y.size(3)); }
+
+// event pool for side-stream fork points
+hipEvent_t next_event() {
+  static std::mutex mu;
+  static std::vector<hipEvent_t> pool;
+  static size_t next = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (pool.empty()) {
+    pool.resize(512);
+    for (auto& e : pool) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  }
+  hipEvent_t e = pool[next];
+  next = (next + 1) % pool.size();
+  return e;
+}
+
+// dW (+)= wgrad(dy, x) into the parameter's gradient sink, on the side stream if given
+void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                const torch::Tensor& sink, int64_t side) {
+  if (side == 0) {
+    conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, true, c10::nullopt, c10::nullopt);
+    return;
+  }
+  hipStream_t main = cur_stream();
+  hipStream_t ss = reinterpret_cast<hipStream_t>(side);
+  hipEvent_t ev = next_event();
+  check_hip(hipEventRecord(ev, main), "hipEventRecord");
+  check_hip(hipStreamWaitEvent(ss, ev, 0), "hipStreamWaitEvent");
+  auto hs = c10::hip::getStreamFromExternal(ss, dy.device().index());
+  c10::hip::HIPCachingAllocator::recordStream(dy.storage().data_ptr(), hs);
+  c10::hip::HIPCachingAllocator::recordStream(x.storage().data_ptr(), hs);
+  c10::hip::HIPStreamGuard guard(hs);
+  conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, true, c10::nullopt, c10::nullopt);
+}
+
+// bn: [gamma, beta, running_mean, running_var] per BN, in the order bn1, bn2, (bn3), (shortcut bn)
+// returns [out, y1, a1, y2, a2, y3|-, ys|-, then sc, sh, mu, iv per BN]
+std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor> w, std::vector<torch::Tensor> bn,
+                                     int64_t stride, bool bottleneck, bool proj, bool training, double eps,
+                                     double momentum) {
+  const int nconv = bottleneck ? 3 : 2;
+  TORCH_CHECK((int)w.size() == nconv + (proj ? 1 : 0), "block_fwd: weight count");
+  TORCH_CHECK(bn.size() == w.size() * 4, "block_fwd: 4 BN tensors per conv");
+  auto B = [&](int i, int k) { return bn[i * 4 + k]; };
+  std::vector<BnState> st;
+  std::vector<torch::Tensor> out(7);
+  const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
+  auto c1 = conv_fwd(x, w[0], s1, p1, training, -1, c10::nullopt, c10::nullopt);
+  const double cnt1 = rows_of(c1[0]);
+  st.push_back(bn_forward(c1[1], cnt1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training));
+  auto a1 = bn_apply(c1[0], st[0].sc, st[0].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true);
+  const int64_t s2 = bottleneck ? stride : 1;
+  auto c2 = conv_fwd(a1, w[1], s2, 1, training, -1, c10::nullopt, c10::nullopt);
+  const double cnt2 = rows_of(c2[0]);
+  st.push_back(bn_forward(c2[1], cnt2, B(1, 0), B(1, 1), B(1, 2), B(1, 3), eps, momentum, training));
+  torch::Tensor last = c2[0], a2;
+  int lastbn = 1;
+  if (bottleneck) {
+    a2 = bn_apply(c2[0], st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true);
+    auto c3 = conv_fwd(a2, w[2], 1, 0, training, -1, c10::nullopt, c10::nullopt);
+    st.push_back(bn_forward(c3[1], cnt2, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training));
+    last = c3[0];
+    lastbn = 2;
+  }
+  torch::Tensor o, ys;
+  if (proj) {
+    auto cs = conv_fwd(x, w[nconv], stride, 0, training, -1, c10::nullopt, c10::nullopt);
+    st.push_back(bn_forward(cs[1], cnt2, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
+                            training));
+    ys = cs[0];
+    o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true);
+  } else {
+    o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, x, c10::nullopt, c10::nullopt, 2, true);
+  }
+  out[0] = o;
+  out[1] = c1[0];
+  out[2] = a1;
+  out[3] = c2[0];
+  out[4] = bottleneck ? a2 : torch::Tensor();
+  out[5] = bottleneck ? last : torch::Tensor();
+  out[6] = ys;
+  for (auto& b : st) {
+    out.push_back(b.sc);
+    out.push_back(b.sh);
+    out.push_back(b.mu);
+    out.push_back(b.iv);
+  }
+  return out;
+}
+
+// saved: [x, y1, a1, y2, a2|-, y3|-, ys|-, out] ; bnst: [sc, sh, mu, iv] per BN (fwd order)
+// wt: dgrad-layout weights (conv order); dw: fp32 gradient sinks (conv order);
+// bng: [gamma, dgamma_sink, dbeta_sink] per BN. Returns dx.
+torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, std::vector<torch::Tensor> bnst,
+                        std::vector<torch::Tensor> wt, std::vector<torch::Tensor> dw, std::vector<torch::Tensor> bng,
+                        int64_t stride, bool bottleneck, bool proj, int64_t side) {
+  const int nconv = bottleneck ? 3 : 2;
+  const int nbn = nconv + (proj ? 1 : 0);
+  TORCH_CHECK((int)wt.size() == nbn && (int)dw.size() == nbn && (int)bng.size() == 3 * nbn &&
+                  (int)bnst.size() == 4 * nbn && saved.size() == 8,
+              "block_bwd: argument counts");
+  const torch::Tensor &x = saved[0], &y1 = saved[1], &a1 = saved[2], &y2 = saved[3], &a2 = saved[4],
+                      &y3 = saved[5], &ys = saved[6], &out = saved[7];
+  auto S = [&](int i, int k) { return bnst[i * 4 + k]; };
+  auto G = [&](int i, int k) { return bng[i * 3 + k]; };
+  const int64_t H = x.size(1), W = x.size(2);
+  const int lastbn = nconv - 1;
+  const torch::Tensor& ylast = bottleneck ? y3 : y2;
+  const double cnt_last = rows_of(ylast), cnt1 = rows_of(y1);
+  torch::Tensor dylast, dys, dz;
+  if (proj) {
+    auto c = bn_bwd_reduce_coef(dout, out, ylast, S(lastbn, 2), ys, S(nconv, 2), c10::nullopt, c10::nullopt,
+                                cnt_last, G(lastbn, 0), S(lastbn, 3), G(nconv, 0), S(nconv, 3), G(lastbn, 1),
+                                G(lastbn, 2), G(nconv, 1), G(nconv, 2));
+    auto r = bn_bwd_apply(dout, out, ylast, c[0], ys, c[1], false, c10::nullopt, c10::nullopt);
+    dylast = r[0];
+    dys = r[1];
+  } else {
+    auto c = bn_bwd_reduce_coef(dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
+                                c10::nullopt, cnt_last, G(lastbn, 0), S(lastbn, 3), c10::nullopt, c10::nullopt,
+                                G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt);
+    auto r = bn_bwd_apply(dout, out, ylast, c[0], c10::nullopt, c10::nullopt, true, c10::nullopt, c10::nullopt);
+    dylast = r[0];
+    dz = r[2];
+  }
+  torch::Tensor dy1;
+  if (bottleneck) {
+    side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
+    auto da2 = conv_dgrad(dylast, wt[2], y2.size(1), y2.size(2), 1, 0, -1, c10::nullopt, c10::nullopt);
+    auto c2 = bn_bwd_reduce_coef(da2, c10::nullopt, y2, S(1, 2), c10::nullopt, c10::nullopt, S(1, 0), S(1, 1),
+                                 cnt_last, G(1, 0), S(1, 3), c10::nullopt, c10::nullopt, G(1, 1), G(1, 2),
+                                 c10::nullopt, c10::nullopt);
+    auto dy2 = bn_bwd_apply(da2, c10::nullopt, y2, c2[0], c10::nullopt, c10::nullopt, false, S(1, 0), S(1, 1))[0];
+    side_wgrad(dy2, a1, 3, 3, stride, 1, dw[1], side);
+    auto da1 = conv_dgrad(dy2, wt[1], H, W, stride, 1, -1, c10::nullopt, c10::nullopt);
+    auto c1 = bn_bwd_reduce_coef(da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
+                                 cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
+                                 c10::nullopt);
+    dy1 = bn_bwd_apply(da1, c10::nullopt, y1, c1[0], c10::nullopt, c10::nullopt, false, S(0, 0), S(0, 1))[0];
+    side_wgrad(dy1, x, 1, 1, 1, 0, dw[0], side);
+  } else {
+    side_wgrad(dylast, a1, 3, 3, 1, 1, dw[1], side);
+    auto da1 = conv_dgrad(dylast, wt[1], y1.size(1), y1.size(2), 1, 1, -1, c10::nullopt, c10::nullopt);
+    auto c1 = bn_bwd_reduce_coef(da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
+                                 cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
+                                 c10::nullopt);
+    dy1 = bn_bwd_apply(da1, c10::nullopt, y1, c1[0], c10::nullopt, c10::nullopt, false, S(0, 0), S(0, 1))[0];
+    side_wgrad(dy1, x, 3, 3, stride, 1, dw[0], side);
+  }
+  const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
+  torch::Tensor dx;
+  if (proj) {
+    side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);
+    dx = conv_dgrad(dys, wt[nconv], H, W, stride, 0, -1, c10::nullopt, c10::nullopt);
+    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, dx, dx);
+  } else {
+    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, c10::nullopt, dz);
+  }
+  return dx;
+}
+
 }  // namespace
 
 void register_conv_bn(pybind11::module& m) {
@@ -573,6 +763,8 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("inv_b") = pybind11::none(), pybind11::arg("sink_ga") = pybind11::none(),
         pybind11::arg("sink_ba") = pybind11::none(), pybind11::arg("sink_gb") = pybind11::none(),
         pybind11::arg("sink_bb") = pybind11::none());
+  m.def("block_fwd", &block_fwd, "native residual-block forward (whole kernel sequence, single-process BN)");
+  m.def("block_bwd", &block_bwd, "native residual-block backward (dgrad chain + side-stream wgrads)");
   m.def("bn_bwd_apply", &bn_bwd_apply, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
         pybind11::arg("ca"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("cb") = pybind11::none(),
         pybind11::arg("want_dz") = false, pybind11::arg("msc") = pybind11::none(),

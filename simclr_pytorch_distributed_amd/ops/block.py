@@ -270,16 +270,97 @@ class _Stem(torch.autograd.Function):
         return (None, None, None, None, None) + (None,) * len(ctx.params)
 
 
+class _NativeBlock(torch.autograd.Function):
+    """Whole residual block through the native executor (csrc/bindings/conv_bn_ops.cpp
+    ``block_fwd`` / ``block_bwd``): one host call per block and direction instead of
+    ~12 / ~20 Python-level kernel calls. Same kernels and math as :class:`_Bottleneck` /
+    :class:`_Basic` (materialised internal activations, ReLU masks from y in backward,
+    side-stream wgrads); used when BN statistics need no cross-rank all-reduce."""
+
+    @staticmethod
+    def forward(ctx, x, blk, wc, training, info, *params):
+        m = _ext.require()
+        convs, bns, bottle, proj = info
+        bn0 = bns[0]
+        bn_list = []
+        for bn in bns:
+            bn_list += [bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var]
+        r = m.block_fwd(x, [wc.fwd(cv) for cv in convs], bn_list, blk.stride, bottle, proj, training, bn0.eps,
+                        bn0.momentum)
+        out = r[0]
+        if training:
+            e = _empty(x)
+            saved = [x] + [t if t is not None else e for t in r[1:7]] + [out]
+            ctx.save_for_backward(*saved, *r[7:])
+            ctx.blk, ctx.wc, ctx.info, ctx.params = blk, wc, info, params
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        m = _ext.require()
+        convs, bns, bottle, proj = ctx.info
+        t = ctx.saved_tensors
+        wc = ctx.wc
+        bng = []
+        for bn in bns:
+            bng += [bn.weight.detach(), sinks.target(bn.weight), sinks.target(bn.bias)]
+        from . import streams
+        side = streams.side(dout.device).cuda_stream if streams.ENABLED else 0
+        dx = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
+                         [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side)
+        sinks.notify(ctx.params)
+        return (dx, None, None, None, None) + (None,) * len(ctx.params)
+
+
+_EMPTY = {}
+
+
+def _empty(like):
+    e = _EMPTY.get(like.device)
+    if e is None:
+        e = _EMPTY[like.device] = torch.empty(0, dtype=like.dtype, device=like.device)
+    return e
+
+
+NATIVE_EXEC = os.environ.get("SDX_NATIVE_EXEC", "1") != "0"
+
+
+def _block_info(blk):
+    """(convs, bns, bottleneck?, projection?) and the parameter list, cached on the module."""
+    info = getattr(blk, "_sdx_info", None)
+    if info is None:
+        bottle = hasattr(blk, "conv3")
+        proj = len(blk.shortcut) > 0
+        convs = [blk.conv1, blk.conv2] + ([blk.conv3] if bottle else []) + ([blk.shortcut[0]] if proj else [])
+        bns = [blk.bn1, blk.bn2] + ([blk.bn3] if bottle else []) + ([blk.shortcut[1]] if proj else [])
+        info = ((convs, bns, bottle, proj), [p for p in blk.parameters()])
+        blk._sdx_info = info
+    return info
+
+
+def _use_native_exec(group, blk_info) -> bool:
+    bns = blk_info[1]
+    return (NATIVE_EXEC and group is None and not FUSE_PROLOGUE and bns[0].momentum is not None
+            and all(bn.affine and bn.track_running_stats for bn in bns))
+
+
 def block_params(mod) -> List[torch.nn.Parameter]:
-    return [p for p in mod.parameters()]
+    info = getattr(mod, "_sdx_info", None)
+    return list(info[1]) if info is not None else [p for p in mod.parameters()]
 
 
 def bottleneck(x, blk, wc, training: bool, group=None):
-    return _Bottleneck.apply(x, blk, wc, training, group, *block_params(blk))
+    info, params = _block_info(blk)
+    if _use_native_exec(group, info):
+        return _NativeBlock.apply(x, blk, wc, training, info, *params)
+    return _Bottleneck.apply(x, blk, wc, training, group, *params)
 
 
 def basic(x, blk, wc, training: bool, group=None):
-    return _Basic.apply(x, blk, wc, training, group, *block_params(blk))
+    info, params = _block_info(blk)
+    if _use_native_exec(group, info):
+        return _NativeBlock.apply(x, blk, wc, training, info, *params)
+    return _Basic.apply(x, blk, wc, training, group, *params)
 
 
 def stem(x, enc, wc, training: bool, group=None):

@@ -83,12 +83,13 @@ def test_native_blocks_teacher_forced(gpu):
 
 
 @pytest.mark.parametrize("name", ["resnet18", "resnet50"])
-@pytest.mark.parametrize("prologue", [True, False])
-def test_fused_blocks_match_unfused(gpu, name, prologue, monkeypatch):
+@pytest.mark.parametrize("variant", ["native_exec", "py_blocks", "py_prologue"])
+def test_fused_blocks_match_unfused(gpu, name, variant, monkeypatch):
     """Fused block autograd (weight cache, grad sinks, fused residual-grad, with/without the
     BN+ReLU conv prologue) == per-op path."""
     from simclr_pytorch_distributed_amd.ops import block
-    monkeypatch.setattr(block, "FUSE_PROLOGUE", prologue)
+    monkeypatch.setattr(block, "FUSE_PROLOGUE", variant == "py_prologue")
+    monkeypatch.setattr(block, "NATIVE_EXEC", variant == "native_exec")
     from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
     from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""cProfile of the host side of the native training step (where do the ~15 ms of Python /
+launch overhead per step go?)."""
+import cProfile
+import os
+import pstats
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    import logging
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    logging.disable(logging.INFO)
+    opt = parse_pretrain(["--batch_size", "256", "--synthetic", "--synthetic_size", "8192", "--backend", "native",
+                          "--work_dir", "/tmp/hp", "--temp", "0.5", "--cosine"], make_dirs=False)
+    eng = PretrainEngine(opt)
+    eng.model.train()
+    eng.sampler.set_epoch(1)
+    idxs = list(eng.sampler.batches(eng.device))
+    for i in range(5):
+        eng.train_step(idxs[i], 1, i, len(idxs))
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    for i in range(20):
+        eng.train_step(idxs[5 + i], 1, 5 + i, len(idxs))
+    pr.disable()
+    torch.cuda.synchronize()
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(35)
+
+
+if __name__ == "__main__":
+    main()
