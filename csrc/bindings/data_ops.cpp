@@ -34,7 +34,7 @@ torch::Tensor gpu_augment(torch::Tensor data, torch::Tensor idx, int64_t S, int6
                                (int)data.size(2), (int)S, (int)n_views, (uint64_t)seed, m, sd, (float)scale_lo,
                                (float)scale_hi, (float)ratio_lo, (float)ratio_hi, (float)jitter_p, (float)bright,
                                (float)contrast, (float)sat, (float)hue, (float)gray_p, do_crop ? 1 : 0,
-                               do_flip ? 1 : 0, sd_dev, out.data_ptr(), cur_stream()),
+                               do_flip ? 1 : 0, sd_dev, out.data_ptr(), cur_stream(), (long)data.size(0)),
             "gpu_augment");
   return out;
 }

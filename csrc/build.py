@@ -8,7 +8,11 @@ Objects are cached under ``build/obj`` keyed on source mtime, included-header mt
 and the flag string, and compiled in parallel. The final shared object is written
 inside the package so it travels to the GPU box with the repo snapshot.
 
-Usage: ``python csrc/build.py [--force] [--jobs N] [--debug]``
+Usage: ``python csrc/build.py [--force] [--jobs N] [--debug] [--checked]``
+
+``--checked`` builds ``_C_checked.so`` with device-side bounds checks (``SDX_DCHECK``:
+every implicit-GEMM operand gather, augmentation source pixel, pooling window) that trap
+with a message on violation; load it with ``SDX_CHECKED=1``.
 """
 from __future__ import annotations
 
@@ -57,7 +61,8 @@ def _sources():
     return kern, bind
 
 
-def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False,
+          checked: bool = False) -> str:
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc_torch, lib_torch, abi = _torch_paths()
     hipcc = _hipcc()
@@ -65,12 +70,14 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = ["-std=c++17", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-Wno-unused-result",
               "-Wno-deprecated-declarations"]
+    name = "_C_checked" if checked else "_C"
+    out_so = os.path.join(PKG, name + ".so")
     kflags = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-              "-ffp-contract=fast"] + opt + common
+              "-ffp-contract=fast"] + opt + common + (["-DSDX_CHECKED=1"] if checked else [])
     bflags = [os.environ.get("CXX", "g++"), "-O2", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               "-I/opt/rocm/include",
               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
-              "-DTORCH_EXTENSION_NAME=_C", f"-I{py_inc}"] + [f"-I{p}" for p in inc_torch] + common
+              f"-DTORCH_EXTENSION_NAME={name}", f"-I{py_inc}"] + [f"-I{p}" for p in inc_torch] + common
     hdr_m = _headers_mtime()
     kern, bind = _sources()
 
@@ -94,30 +101,32 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         results = list(ex.map(lambda t: job(*t), tasks))
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
-    if rebuilt or force or not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs):
+    if (rebuilt or force or not os.path.exists(out_so)
+            or os.path.getmtime(out_so) < max(os.path.getmtime(o) for o in objs)):
         libs = []
         for p in lib_torch:
             libs += [f"-L{p}", f"-Wl,-rpath,{p}"]
         libs += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
-        tmp = OUT + ".tmp"
+        tmp = out_so + ".tmp"
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + libs
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, OUT)
-    return OUT
+        os.replace(tmp, out_so)
+    return out_so
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--checked", action="store_true", help="device bounds checks -> _C_checked.so")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
-    out = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose)
+    out = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose, checked=a.checked)
     print(out)
 
 

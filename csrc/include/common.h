@@ -8,6 +8,23 @@
 #include <stdint.h>
 #include <type_traits>
 
+// Device-side checks, compiled in only for the checked build (csrc/build.py --checked):
+// a violated condition prints its location and traps the wave.
+#ifdef SDX_CHECKED
+#define SDX_DCHECK(cond)                                                                    \
+  do {                                                                                      \
+    if (!(cond)) {                                                                          \
+      printf("SDX_DCHECK failed %s:%d: %s (block %d thread %d)\n", __FILE__, __LINE__, #cond, \
+             (int)blockIdx.x, (int)threadIdx.x);                                            \
+      __builtin_trap();                                                                     \
+    }                                                                                       \
+  } while (0)
+#else
+#define SDX_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace sdx {
 
 constexpr int kWave = 64;   // CDNA wavefront width (never 32)

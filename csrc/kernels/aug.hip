@@ -36,6 +36,7 @@ struct Rng {
 
 struct AugParams {
   const uint8_t* data;     // [n_data][H][W][3]
+  long n_data;             // images in `data` (bounds checks)
   const int64_t* idx;      // [B]
   uint16_t* out;           // [n_views*B][S][S][8]
   int B, H, W, S, n_views;
@@ -140,6 +141,7 @@ __device__ void sample_pixel(const AugParams& p, const uint8_t* img, const ViewP
   const int y0 = (int)floorf(sy), x0 = (int)floorf(sx);
   const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
   const float wy = sy - y0, wx = sx - x0;
+  SDX_DCHECK(y0 >= 0 && x0 >= 0 && y0 < p.H && x0 < p.W && y1 < p.H && x1 < p.W);
   const uint8_t* p00 = img + ((size_t)y0 * p.W + x0) * 3;
   const uint8_t* p01 = img + ((size_t)y0 * p.W + x1) * 3;
   const uint8_t* p10 = img + ((size_t)y1 * p.W + x0) * 3;
@@ -181,6 +183,7 @@ __global__ __launch_bounds__(256) void aug_kernel(AugParams p) {
   __shared__ ViewParams vp;
   const int b = blockIdx.x, view = blockIdx.y;
   const int64_t src = p.idx[b];
+  SDX_DCHECK(p.n_data <= 0 || (src >= 0 && src < p.n_data));
   const uint8_t* img = p.data + (size_t)src * p.H * p.W * 3;
   if (threadIdx.x == 0) {
     const uint64_t seed = p.seed_dev ? (uint64_t)p.seed_dev[0] : p.seed;
@@ -228,9 +231,9 @@ hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, in
                               uint64_t seed, const float* mean, const float* std, float scale_lo, float scale_hi,
                               float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
                               float sat, float hue, float gray_p, int do_crop, int do_flip, const int64_t* seed_dev,
-                              void* out,
-                              hipStream_t s) {
+                              void* out, hipStream_t s, long n_data) {
   AugParams p{};
+  p.n_data = n_data;
   p.data = data; p.idx = idx; p.out = (uint16_t*)out;
   p.B = B; p.H = H; p.W = W; p.S = S; p.n_views = n_views; p.seed = seed;
   for (int k = 0; k < 3; ++k) { p.mean[k] = mean[k]; p.inv_std[k] = 1.f / std[k]; }

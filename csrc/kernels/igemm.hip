@@ -51,6 +51,8 @@ struct IgemmParams {
   // diagnostic ablation (SDX_IGEMM_ABLATE bits, timing only — results are wrong):
   // 1 skip LDS stores, 2 skip global loads, 4 skip MFMAs
   int ablate;
+  // operand sizes in elements (bounds checks of the checked build)
+  long a_elems, b_elems;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -297,11 +299,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
           ok = kok && (unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q;
           off = a_base[i] + (ty * g.Q + tx) * g.K + kc;
         }
+        SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
         ra[i] = ld16_or_zero(p.a + off, ok);
       }
       // B: weights [Ncol][Kdim] K-contiguous
 #pragma unroll
-      for (int i = 0; i < T::B_CH; ++i) rb[i] = ld16_or_zero(p.b + b_off[i] + k, kok && b_off[i] >= 0);
+      for (int i = 0; i < T::B_CH; ++i) {
+        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + k + 8 <= p.b_elems);
+        rb[i] = ld16_or_zero(p.b + b_off[i] + k, kok && b_off[i] >= 0);
+      }
       // advance the k decode by one tile
       kc += BK;
       while (kc >= cdim) {
@@ -315,6 +321,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         const int e = tid + 256 * i;
         const int row = e / A_CPR, ch = e % A_CPR;
         const int kk = k0 + row, co = m0 + ch * 8;
+        SDX_DCHECK(!(kk < k_end && co < p.M) || (long)kk * g.K + co + 8 <= p.a_elems);
         ra[i] = ld16_or_zero(p.a + kk * g.K + co, kk < k_end && co < p.M);
       }
       // WGRAD B: im2col(x) rows (pixels) x BN (r,s,ci); the column chunk is fixed per thread
@@ -338,6 +345,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
           off = ((n * g.H + yy) * g.W + xx) * g.C + wb_c;
         }
         if (ok) ld_mask |= 1u << i;
+        SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.b_elems));
         rb[i] = ld16_or_zero(p.b + off, ok);
       }
     }
@@ -356,6 +364,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         const int ch = phys ^ kout_swz<BM>(row);
         const int kk = k0 + row, co = m0 + ch * 8;
         const bool ok = kk < k_end && co < p.M;
+        SDX_DCHECK(!ok || (long)kk * g.K + co + 8 <= p.a_elems);
         const uint16_t* src = ok ? p.a + kk * g.K + co : g_zero16;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sa + (wvu * T::A_CH + i) * 1024),
@@ -378,6 +387,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
           ok = ok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
           off = ((n * g.H + yy) * g.W + xx) * g.C + gb_c[i];
         }
+        SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.b_elems));
         const uint16_t* src = ok ? p.b + off : g_zero16;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + (wvu * T::B_CH + i) * 1024),
@@ -405,6 +415,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         ok = kok && (unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q;
         off = a_base[i] + (ty * g.Q + tx) * g.K + kc;
       }
+      SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
       const uint16_t* src = ok ? p.a + off : g_zero16;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
@@ -413,6 +424,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const bool ok = kok && b_off[i] >= 0;
+      SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
       const uint16_t* src = ok ? p.b + b_off[i] + k : g_zero16;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
@@ -812,6 +824,8 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
   p.M = g.N * g.P * g.Q;
   p.Ncol = g.K;
   p.Kdim = g.R * g.S * g.C;
+  p.a_elems = (long)g.N * g.H * g.W * g.C;
+  p.b_elems = (long)p.Ncol * p.Kdim;
   return launch_any<MODE_FWD>(p, cfg, s);
 }
 
@@ -840,6 +854,8 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   if (p.M == 0) return hipSuccess;
   p.Ncol = g.C;
   p.Kdim = p.nr * p.ns * g.K;
+  p.a_elems = (long)g.N * g.P * g.Q * g.K;
+  p.b_elems = (long)p.Ncol * p.Kdim;
   return launch_any<MODE_DGRAD>(p, cfg, s);
 }
 
@@ -863,6 +879,8 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
   p.M = g.K;
   p.Ncol = g.R * g.S * g.C;
   p.Kdim = g.N * g.P * g.Q;
+  p.a_elems = (long)g.N * g.P * g.Q * g.K;
+  p.b_elems = (long)g.N * g.H * g.W * g.C;
   if (splits < 1) splits = 1;
   int per = (p.Kdim + splits - 1) / splits;
   per = ((per + BK - 1) / BK) * BK;

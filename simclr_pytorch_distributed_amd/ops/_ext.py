@@ -50,7 +50,9 @@ def ext():
                     _b.build()
                 finally:
                     sys.path.pop(0)
-            _mod = importlib.import_module("simclr_pytorch_distributed_amd._C")
+            # SDX_CHECKED=1: the bounds-checked build (csrc/build.py --checked)
+            name = "_C_checked" if os.environ.get("SDX_CHECKED", "0") == "1" else "_C"
+            _mod = importlib.import_module("simclr_pytorch_distributed_amd." + name)
         except Exception as e:  # noqa: BLE001
             _err = e
             _mod = None
