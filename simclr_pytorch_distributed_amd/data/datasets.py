@@ -81,13 +81,17 @@ def load_cifar(name: str, root: str, train: bool = True) -> ArrayDataset:
     return ArrayDataset(x, y, spec["ncls"], name)
 
 
-def synthetic_dataset(n: int = 50000, size: int = 32, num_classes: int = 10, seed: int = 0) -> ArrayDataset:
+def synthetic_dataset(n: int = 50000, size: int = 32, num_classes: int = 10, seed: int = 0,
+                      class_seed: int = 0) -> ArrayDataset:
     """CIFAR-shaped random images with class-dependent colour/texture statistics, so a
-    linear probe on learned features has a signal (plumbing/accuracy smoke tests)."""
+    linear probe on learned features has a signal (plumbing/accuracy smoke tests).
+    The per-class statistics come from ``class_seed`` (shared by the train and validation
+    splits); ``seed`` draws the labels and the per-image noise."""
+    crng = np.random.default_rng(1_000_003 + class_seed)
+    base = crng.integers(30, 225, size=(num_classes, 1, 1, 3))
+    freq = crng.uniform(0.2, 1.2, size=(num_classes,))
     rng = np.random.default_rng(seed)
     labels = rng.integers(0, num_classes, size=n).astype(np.int64)
-    base = rng.integers(30, 225, size=(num_classes, 1, 1, 3))
-    freq = rng.uniform(0.2, 1.2, size=(num_classes,))
     yy, xx = np.mgrid[0:size, 0:size]
     imgs = np.empty((n, size, size, 3), dtype=np.uint8)
     chunk = 4096
@@ -130,7 +134,7 @@ def build_dataset(dataset: str, data_folder: str, train: bool = True, synthetic:
     if synthetic:
         ncls = {"cifar10": 10, "cifar100": 100}.get(dataset, 10)
         n = synthetic_size if train else max(1000, synthetic_size // 5)
-        return synthetic_dataset(n, size if dataset == "path" else 32, ncls, seed + (0 if train else 1))
+        return synthetic_dataset(n, size if dataset == "path" else 32, ncls, seed + (0 if train else 1), class_seed=seed)
     if dataset in _CIFAR:
         return load_cifar(dataset, data_folder, train)
     if dataset == "path":
