@@ -321,8 +321,14 @@ std::vector<torch::Tensor> bn_eval_affine(OptT gamma, OptT beta, torch::Tensor r
   return {scale, shift};
 }
 
+// ReLU bitmask of an activation: uint8 [numel/8], bit i of byte e = value 8e+i > 0
+void check_mask(const torch::Tensor& m, int64_t numel, const char* name) {
+  TORCH_CHECK(m.is_cuda() && m.scalar_type() == at::kByte && m.is_contiguous() && m.numel() * 8 == numel, name,
+              " must be a contiguous uint8 GPU tensor of numel/8 bytes");
+}
+
 torch::Tensor bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, OptT r, OptT scale2, OptT shift2,
-                       int64_t res_mode, bool relu) {
+                       int64_t res_mode, bool relu, OptT mask_out) {
   check_bf16_nhwc(y, "y");
   const int64_t C = y.size(3);
   check_vec(scale, C, "scale");
@@ -343,8 +349,13 @@ torch::Tensor bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift
   }
   c10::DeviceGuard dg(y.device());
   auto out = torch::empty_like(y);
+  void* mp = nullptr;
+  if (mask_out.has_value()) {
+    check_mask(*mask_out, y.numel(), "mask_out");
+    mp = mask_out->data_ptr();
+  }
   check_hip(launch_bn_apply(y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, s2, t2, (int)res_mode,
-                            relu ? 1 : 0, out.data_ptr(), y.numel(), C, cur_stream()),
+                            relu ? 1 : 0, out.data_ptr(), y.numel(), C, cur_stream(), mp),
             "bn_apply");
   return out;
 }
@@ -355,6 +366,7 @@ void check_bwd_C(int64_t C) {
 
 struct BwdIn {
   const void* op = nullptr;
+  const void* om = nullptr;   // ReLU bitmask instead of the activation
   const void* ybp = nullptr;
   const float* mbp = nullptr;
   const float* mk_s = nullptr;
@@ -372,9 +384,14 @@ BwdIn bwd_inputs(const torch::Tensor& dout, const OptT& outv, const torch::Tenso
   TORCH_CHECK(ya.sizes() == dout.sizes(), "ya shape");
   check_vec(ma, in.C, "mean_a");
   if (outv.has_value()) {
-    check_bf16_nhwc(*outv, "out");
-    TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
-    in.op = outv->data_ptr();
+    if (outv->scalar_type() == at::kByte) {
+      check_mask(*outv, dout.numel(), "out (bitmask)");
+      in.om = outv->data_ptr();
+    } else {
+      check_bf16_nhwc(*outv, "out");
+      TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
+      in.op = outv->data_ptr();
+    }
   }
   if (yb.has_value()) {
     check_bf16_nhwc(*yb, "yb");
@@ -403,7 +420,7 @@ torch::Tensor bn_bwd_reduce(torch::Tensor dout, OptT outv, torch::Tensor ya, tor
   check_hip(launch_bn_bwd_reduce(dout.data_ptr(), in.op, ya.data_ptr(), ma.data_ptr<float>(), in.ybp, in.mbp,
                                  dout.numel(), C, partial.data_ptr<float>(), scratch.data_ptr<double>(),
                                  reduce_counters(dout.device()), sums.data_ptr<double>(), 0, nullptr, cur_stream(),
-                                 in.mk_s, in.mk_t),
+                                 in.mk_s, in.mk_t, in.om),
             "bn_bwd_reduce");
   return sums;
 }
@@ -497,7 +514,7 @@ std::vector<torch::Tensor> bn_bwd_reduce_coef(torch::Tensor dout, OptT outv, tor
   check_hip(launch_bn_bwd_reduce(dout.data_ptr(), in.op, ya.data_ptr(), ma.data_ptr<float>(), in.ybp, in.mbp,
                                  dout.numel(), C, partial.data_ptr<float>(), scratch.data_ptr<double>(),
                                  reduce_counters(dout.device()), sums.data_ptr<double>(), 2, &a, cur_stream(),
-                                 in.mk_s, in.mk_t),
+                                 in.mk_s, in.mk_t, in.om),
             "bn_bwd_reduce_coef");
   return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
 }
@@ -510,10 +527,16 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
   TORCH_CHECK(ya.sizes() == dout.sizes(), "ya shape");
   TORCH_CHECK(ca.is_cuda() && ca.scalar_type() == at::kFloat && ca.numel() == 3 * C && ca.is_contiguous(), "coef_a");
   const void* op = nullptr;
+  const void* om = nullptr;
   if (outv.has_value()) {
-    check_bf16_nhwc(*outv, "out");
-    TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
-    op = outv->data_ptr();
+    if (outv->scalar_type() == at::kByte) {
+      check_mask(*outv, dout.numel(), "out (bitmask)");
+      om = outv->data_ptr();
+    } else {
+      check_bf16_nhwc(*outv, "out");
+      TORCH_CHECK(outv->sizes() == dout.sizes(), "out shape");
+      op = outv->data_ptr();
+    }
   }
   c10::DeviceGuard dg(dout.device());
   auto dya = torch::empty_like(dout);
@@ -535,7 +558,7 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
   dz = want_dz ? torch::empty_like(dout) : torch::empty({0}, dout.options());
   check_hip(launch_bn_bwd_apply(dout.data_ptr(), op, ya.data_ptr(), ca.data_ptr<float>(), ybp, cbp, dya.data_ptr(),
                                 ybp ? dyb.data_ptr() : nullptr, want_dz ? dz.data_ptr() : nullptr, dout.numel(), C,
-                                cur_stream(), mk_s, mk_t),
+                                cur_stream(), mk_s, mk_t, om),
             "bn_bwd_apply");
   return {dya, dyb, dz};
 }
@@ -601,7 +624,8 @@ void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int6
 }
 
 // bn: [gamma, beta, running_mean, running_var] per BN, in the order bn1, bn2, (bn3), (shortcut bn)
-// returns [out, y1, a1, y2, a2, y3|-, ys|-, then sc, sh, mu, iv per BN]
+// returns [out, y1, a1, y2, a2|-, y3|-, ys|-, omask (uint8 ReLU bits of out; training only),
+//          then sc, sh, mu, iv per BN]
 std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor> w, std::vector<torch::Tensor> bn,
                                      int64_t stride, bool bottleneck, bool proj, bool training, double eps,
                                      double momentum) {
@@ -615,7 +639,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   auto c1 = conv_fwd(x, w[0], s1, p1, training, -1, c10::nullopt, c10::nullopt);
   const double cnt1 = rows_of(c1[0]);
   st.push_back(bn_forward(c1[1], cnt1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training));
-  auto a1 = bn_apply(c1[0], st[0].sc, st[0].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true);
+  auto a1 = bn_apply(c1[0], st[0].sc, st[0].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
   const int64_t s2 = bottleneck ? stride : 1;
   auto c2 = conv_fwd(a1, w[1], s2, 1, training, -1, c10::nullopt, c10::nullopt);
   const double cnt2 = rows_of(c2[0]);
@@ -623,22 +647,27 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   torch::Tensor last = c2[0], a2;
   int lastbn = 1;
   if (bottleneck) {
-    a2 = bn_apply(c2[0], st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true);
+    a2 = bn_apply(c2[0], st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
     auto c3 = conv_fwd(a2, w[2], 1, 0, training, -1, c10::nullopt, c10::nullopt);
     st.push_back(bn_forward(c3[1], cnt2, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training));
     last = c3[0];
     lastbn = 2;
   }
   torch::Tensor o, ys;
+  // the block output's ReLU mask for backward: 1 bit per element instead of re-reading out
+  torch::Tensor omask = training ? torch::empty({last.numel() / 8}, last.options().dtype(at::kByte))
+                                 : torch::Tensor();
+  const OptT om = training ? OptT(omask) : OptT();
   if (proj) {
     auto cs = conv_fwd(x, w[nconv], stride, 0, training, -1, c10::nullopt, c10::nullopt);
     st.push_back(bn_forward(cs[1], cnt2, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
                             training));
     ys = cs[0];
-    o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true);
+    o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true, om);
   } else {
-    o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, x, c10::nullopt, c10::nullopt, 2, true);
+    o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, x, c10::nullopt, c10::nullopt, 2, true, om);
   }
+  out.push_back(omask);    // index 7 (before the per-BN state)
   out[0] = o;
   out[1] = c1[0];
   out[2] = a1;
@@ -646,6 +675,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   out[4] = bottleneck ? a2 : torch::Tensor();
   out[5] = bottleneck ? last : torch::Tensor();
   out[6] = ys;
+  // layout: [out, y1, a1, y2, a2, y3, ys, omask, then sc, sh, mu, iv per BN]
   for (auto& b : st) {
     out.push_back(b.sc);
     out.push_back(b.sh);
@@ -655,7 +685,8 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   return out;
 }
 
-// saved: [x, y1, a1, y2, a2|-, y3|-, ys|-, out] ; bnst: [sc, sh, mu, iv] per BN (fwd order)
+// saved: [x, y1, a1, y2, a2|-, y3|-, ys|-, out or its uint8 ReLU bitmask] ;
+// bnst: [sc, sh, mu, iv] per BN (fwd order)
 // wt: dgrad-layout weights (conv order); dw: fp32 gradient sinks (conv order);
 // bng: [gamma, dgamma_sink, dbeta_sink] per BN. Returns dx.
 torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, std::vector<torch::Tensor> bnst,
@@ -746,7 +777,10 @@ void register_conv_bn(pybind11::module& m) {
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_stats_finalize", &bn_stats_finalize, "conv stat slab -> BN affine in one launch");
   m.def("bn_eval_affine", &bn_eval_affine);
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, pybind11::arg("y"), pybind11::arg("scale"), pybind11::arg("shift"),
+        pybind11::arg("r") = pybind11::none(), pybind11::arg("scale2") = pybind11::none(),
+        pybind11::arg("shift2") = pybind11::none(), pybind11::arg("res_mode") = 0, pybind11::arg("relu") = true,
+        pybind11::arg("mask_out") = pybind11::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
         pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("mb") = pybind11::none(),
         pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none());

@@ -74,18 +74,19 @@ hipError_t launch_bn_finalize(const double* sums, int C, const BnFinalizeArgs& a
 hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                                  float eps, float* scale, float* shift, hipStream_t s);
 hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, const void* r, const float* sc2,
-                           const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s);
+                           const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s,
+                           void* mask_out = nullptr);   // optional uint8 [numel/8]: bit i = out[8e+i] > 0
 int bn_bwd_reduce_blocks(long numel, int C);
 // partial [bn_bwd_reduce_blocks][nsets][C] written by the elementwise pass, then reduced
 // by launch_col_reduce (epi 0: sums only; epi 2: fused coefficients from `ca`)
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
                                 const float* mb, long numel, int C, float* partial, double* scratch,
                                 unsigned* counters, double* sums, int epi, const BnCoefArgs* ca, hipStream_t s,
-                                const float* msc = nullptr, const float* msh = nullptr);
+                                const float* msc = nullptr, const float* msh = nullptr, const void* omask = nullptr);
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, const BnCoefArgs& a, hipStream_t s);
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
                                const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s,
-                               const float* msc = nullptr, const float* msh = nullptr);
+                               const float* msc = nullptr, const float* msh = nullptr, const void* omask = nullptr);
 
 // ---- GPU augmentation (aug.hip) -------------------------------------------------
 hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, int H, int W, int S, int n_views,

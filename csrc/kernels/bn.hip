@@ -210,6 +210,20 @@ __device__ __forceinline__ void load8c(const float* __restrict__ p, float (&v)[8
 // 32-bit indexing (tensors < 2^31 elements). When the grid stride is a multiple of C/8
 // (always for power-of-two C <= 2048) the channel group is fixed per thread: the per-channel
 // coefficients are loaded once into registers.
+// 1 bit per element of 8 packed bf16: set iff the value is > 0 (the ReLU mask of a block
+// output, kept for backward at 1/16 of the activation's bytes)
+__device__ __forceinline__ uint8_t relu_bits(uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo = w[q] & 0xffffu, hi = w[q] >> 16;
+    b |= (uint32_t)((lo & 0x7fffu) != 0 && !(lo & 0x8000u)) << (2 * q);
+    b |= (uint32_t)((hi & 0x7fffu) != 0 && !(hi & 0x8000u)) << (2 * q + 1);
+  }
+  return (uint8_t)b;
+}
+
 template <int RES, bool RELU>
 struct ApplyOp {
   float ss[8], tt[8], aa[8], bb[8];
@@ -244,7 +258,8 @@ template <int RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ sc,
                                                        const float* __restrict__ sh, const uint16_t* __restrict__ r,
                                                        const float* __restrict__ sc2, const float* __restrict__ sh2,
-                                                       uint16_t* __restrict__ out, long n8l, int C8) {
+                                                       uint16_t* __restrict__ out, long n8l, int C8,
+                                                       uint8_t* __restrict__ mask_out) {
   const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
   const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4* Y = reinterpret_cast<const uint4*>(y);
@@ -253,11 +268,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
   ApplyOp<RES, RELU> op;
   if ((stride % C8) == 0) {
     op.load(sc, sh, sc2, sh2, (e0 % C8) * 8);
-    for (int e = e0; e < n8; e += stride) O[e] = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+    for (int e = e0; e < n8; e += stride) {
+      const uint4 o = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+      O[e] = o;
+      if (mask_out) mask_out[e] = relu_bits(o);
+    }
   } else {
     for (int e = e0; e < n8; e += stride) {
       op.load(sc, sh, sc2, sh2, (e % C8) * 8);
-      O[e] = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+      const uint4 o = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+      O[e] = o;
+      if (mask_out) mask_out[e] = relu_bits(o);
     }
   }
 }
@@ -271,7 +292,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ yb, const float* __restrict__ mb,
                                                             long n8, int C8, int C, float* __restrict__ partial,
                                                             const float* __restrict__ msc,
-                                                            const float* __restrict__ msh) {
+                                                            const float* __restrict__ msh,
+                                                            const uint8_t* __restrict__ omask) {
   constexpr int NS = TWO ? 3 : 2;
   __shared__ float red[NS][256][8];
   const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -286,7 +308,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
   // ReLU mask recomputed from the BN input when the activation itself was never stored
   // (its consumer applied BN+ReLU in its load prologue): out > 0  <=>  ya·msc + msh > 0
-  const bool mask_y = outv == nullptr && msc != nullptr;
+  const bool mask_y = outv == nullptr && omask == nullptr && msc != nullptr;
   float mks[8], mkt[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -298,11 +320,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   const uint4* OV = reinterpret_cast<const uint4*>(outv);
   const uint4* YA = reinterpret_cast<const uint4*>(ya);
   const uint4* YB = reinterpret_cast<const uint4*>(yb);
-  auto accum = [&](uint4 dv, uint4 ov, uint4 av, uint4 bv) {
+  auto accum = [&](uint4 dv, uint4 ov, uint4 av, uint4 bv, uint32_t mbits) {
     float d[8], a[8];
     unpack8(dv, d);
     unpack8(av, a);
-    if (outv) {
+    if (omask) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = (mbits >> i) & 1u ? d[i] : 0.f;
+    } else if (outv) {
       float o[8];
       unpack8(ov, o);
 #pragma unroll
@@ -325,7 +350,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   };
   const uint4 z = make_uint4(0, 0, 0, 0);
   // (a 2-chunk unrolled trip measured slower on the 256-channel layer-1 tensors)
-  for (long e = tid; e < n8; e += stride) accum(D[e], outv ? OV[e] : z, YA[e], TWO ? YB[e] : z);
+  for (long e = tid; e < n8; e += stride)
+    accum(D[e], outv ? OV[e] : z, YA[e], TWO ? YB[e] : z, omask ? (uint32_t)omask[e] : 0u);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     red[0][threadIdx.x][i] = s0[i];
@@ -375,7 +401,7 @@ struct BwdApplyOp {
       load8c(cb + C + c0, D2);
       load8c(cb + 2 * C + c0, E2);
     }
-    use_mask = msc != nullptr;
+    use_mask = msc != nullptr;   // (an explicit bitmask takes precedence, see run())
     if (use_mask) {
       load8c(msc + c0, ms);
       load8c(msh + c0, mt);
@@ -383,11 +409,15 @@ struct BwdApplyOp {
   }
   // returns dz (masked dout) in d, writes dya / dyb values
   __device__ __forceinline__ void run(uint4 dv, uint4 ov, bool has_out, uint4 av, uint4 bv, float (&d)[8],
-                                      uint4& ra, uint4& rb) const {
+                                      uint4& ra, uint4& rb, const uint8_t* omask, int e) const {
     float a[8], r[8];
     unpack8(dv, d);
     unpack8(av, a);
-    if (has_out) {
+    if (omask) {
+      const uint32_t mb = omask[e];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
+    } else if (has_out) {
       float o[8];
       unpack8(ov, o);
 #pragma unroll
@@ -416,7 +446,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            uint16_t* __restrict__ dya, uint16_t* __restrict__ dyb,
                                                            uint16_t* __restrict__ dz_out, long n8l, int C8, int C,
                                                            const float* __restrict__ msc,
-                                                           const float* __restrict__ msh) {
+                                                           const float* __restrict__ msh,
+                                                           const uint8_t* __restrict__ omask) {
   const int n8 = (int)n8l, stride = gridDim.x * blockDim.x;
   const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4* D = reinterpret_cast<const uint4*>(dout);
@@ -432,7 +463,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   auto one = [&](int e, uint4 dv, uint4 ov, uint4 av, uint4 bv) {
     float d[8];
     uint4 ra, rb;
-    op.run(dv, ov, has_out, av, bv, d, ra, rb);
+    op.run(dv, ov, has_out, av, bv, d, ra, rb, omask, e);
     if (DZ) DZ[e] = pack8(d);
     DA[e] = ra;
     if (TWO) DB[e] = rb;
@@ -500,14 +531,16 @@ hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, c
 }
 
 hipError_t launch_bn_apply(const void* y, const float* sc, const float* sh, const void* r, const float* sc2,
-                           const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s) {
+                           const float* sh2, int res_mode, int relu, void* out, long numel, int C, hipStream_t s,
+                           void* mask_out) {
   const long n8 = numel / 8;
   const int C8 = C / 8;
   const dim3 grid(ew_grid(n8)), blk(256);
   const uint16_t* yy = (const uint16_t*)y;
   const uint16_t* rr = (const uint16_t*)r;
   uint16_t* oo = (uint16_t*)out;
-#define SDX_APPLY(RM, RL) hipLaunchKernelGGL((bn_apply_kernel<RM, RL>), grid, blk, 0, s, yy, sc, sh, rr, sc2, sh2, oo, n8, C8)
+#define SDX_APPLY(RM, RL) \
+  hipLaunchKernelGGL((bn_apply_kernel<RM, RL>), grid, blk, 0, s, yy, sc, sh, rr, sc2, sh2, oo, n8, C8, (uint8_t*)mask_out)
   if (res_mode == 0) { if (relu) SDX_APPLY(0, true); else SDX_APPLY(0, false); }
   else if (res_mode == 1) { if (relu) SDX_APPLY(1, true); else SDX_APPLY(1, false); }
   else { if (relu) SDX_APPLY(2, true); else SDX_APPLY(2, false); }
@@ -528,7 +561,7 @@ int bn_bwd_reduce_blocks(long numel, int C) {
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
                                 const float* mb, long numel, int C, float* partial, double* scratch,
                                 unsigned* counters, double* sums, int epi, const BnCoefArgs* ca, hipStream_t s,
-                                const float* msc, const float* msh) {
+                                const float* msc, const float* msh, const void* omask) {
   const int nsets = yb ? 3 : 2;
   const long n8 = numel / 8;
   const int C8 = C / 8;
@@ -537,11 +570,11 @@ hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* 
   if (yb)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)yb, mb, n8, C8, C, partial,
-                       msc, msh);
+                       msc, msh, (const uint8_t*)omask);
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3(g), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)nullptr, (const float*)nullptr,
-                       n8, C8, C, partial, msc, msh);
+                       n8, C8, C, partial, msc, msh, (const uint8_t*)omask);
   SDX_LAUNCH_CHECK();
   return launch_col_reduce(partial, g, nsets, C, scratch, counters, sums, epi, nullptr, ca, s);
 }
@@ -554,17 +587,18 @@ hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, const BnCoef
 
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
                                const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s,
-                               const float* msc, const float* msh) {
+                               const float* msc, const float* msh, const void* omask) {
   const long n8 = numel / 8;
   const int C8 = C / 8;
   if (yb)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)yb, cb, (uint16_t*)dya,
-                       (uint16_t*)dyb, (uint16_t*)dz_out, n8, C8, C, msc, msh);
+                       (uint16_t*)dyb, (uint16_t*)dz_out, n8, C8, C, msc, msh, (const uint8_t*)omask);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)nullptr, (const float*)nullptr,
-                       (uint16_t*)dya, (uint16_t*)nullptr, (uint16_t*)dz_out, n8, C8, C, msc, msh);
+                       (uint16_t*)dya, (uint16_t*)nullptr, (uint16_t*)dz_out, n8, C8, C, msc, msh,
+                       (const uint8_t*)omask);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

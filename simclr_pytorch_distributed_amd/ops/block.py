@@ -290,8 +290,9 @@ class _NativeBlock(torch.autograd.Function):
         out = r[0]
         if training:
             e = _empty(x)
-            saved = [x] + [t if t is not None else e for t in r[1:7]] + [out]
-            ctx.save_for_backward(*saved, *r[7:])
+            # r[7]: the block output's ReLU bitmask (1 bit/element) replaces `out` in backward
+            saved = [x] + [t if t is not None else e for t in r[1:7]] + [r[7]]
+            ctx.save_for_backward(*saved, *r[8:])
             ctx.blk, ctx.wc, ctx.info, ctx.params = blk, wc, info, params
         return out
 

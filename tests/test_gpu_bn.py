@@ -161,3 +161,27 @@ def test_bwd_reduce_coef_fused(gpu, two):
     m.bn_bwd_reduce_coef(dout, out, y, mu, yb, mb, None, None, cnt, g1, inv, g2 if two else None,
                          inv2 if two else None, **kw)
     assert torch.allclose(sga, ref[2] + 1) and torch.allclose(sba, ref[3] + 1)
+
+
+def test_relu_bitmask_matches_activation(gpu):
+    """bn_apply(mask_out=) writes the ReLU bits of its output; the backward kernels give
+    identical results from the bitmask and from the bf16 activation."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(5)
+    N, H, W, C = 4, 8, 8, 256
+    y = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    r = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    mask = torch.empty(y.numel() // 8, dtype=torch.uint8, device=gpu)
+    out = m.bn_apply(y, sc, sh, r, None, None, 2, True, mask_out=mask)
+    bits = ((mask.long().unsqueeze(1) >> torch.arange(8, device=gpu)) & 1).reshape(-1)
+    assert torch.equal(bits.bool(), (out.reshape(-1).float() > 0))
+    d = torch.randn_like(out)
+    mu, iv = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    s1, s2 = m.bn_bwd_reduce(d, out, y, mu), m.bn_bwd_reduce(d, mask, y, mu)
+    assert torch.equal(s1, s2)
+    ca = m.bn_bwd_coef(s1, float(N * H * W), sc, mu, iv)[0]
+    a1 = m.bn_bwd_apply(d, out, y, ca, None, None, True)
+    a2 = m.bn_bwd_apply(d, mask, y, ca, None, None, True)
+    assert torch.equal(a1[0], a2[0]) and torch.equal(a1[2], a2[2])
