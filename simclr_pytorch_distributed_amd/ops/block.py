@@ -38,6 +38,14 @@ from .streams import SideWork
 FUSE_PROLOGUE = os.environ.get("SDX_FUSE_PROLOGUE", "0") == "1"
 
 
+def _omask(like, training):
+    """uint8 ReLU bitmask buffer (1 bit per element) for a block output, training only:
+    BN backward reads it instead of the bf16 output."""
+    if not training:
+        return None
+    return torch.empty(like.numel() // 8, dtype=torch.uint8, device=like.device)
+
+
 def _world(group) -> int:
     return dist.get_world_size(group) if group is not None else 1
 
@@ -134,12 +142,15 @@ class _Bottleneck(torch.autograd.Function):
         if proj:
             ys, ss = _conv(m, x, wc.fwd(blk.shortcut[0]), st, 0, training)
             scs, shs, mus, ivs = _BN.forward(m, ss, blk.shortcut[1], cnt2, training, group)
-            out = m.bn_apply(y3, sc3, sh3, ys, scs, shs, 1, True)
+            om = _omask(y3, training)
+            out = m.bn_apply(y3, sc3, sh3, ys, scs, shs, 1, True, mask_out=om)
         else:
-            out = m.bn_apply(y3, sc3, sh3, x, None, None, 2, True)
+            om = _omask(y3, training)
+            out = m.bn_apply(y3, sc3, sh3, x, None, None, 2, True, mask_out=om)
         if training:
             fused = f1 is not None
-            ctx.save_for_backward(x, y1, None if fused else a1, y2, None if fused else a2, y3, ys, out, mu1, iv1,
+            # the output's 1-bit ReLU mask stands in for `out` in backward
+            ctx.save_for_backward(x, y1, None if fused else a1, y2, None if fused else a2, y3, ys, om, mu1, iv1,
                                   mu2, iv2, mu3, iv3, mus, ivs, sc1, sh1, sc2, sh2)
             ctx.blk, ctx.wc, ctx.group, ctx.params = blk, wc, group, params
             ctx.cnt = (cnt1, cnt2)
@@ -196,11 +207,13 @@ class _Basic(torch.autograd.Function):
         if proj:
             ys, ss = _conv(m, x, wc.fwd(blk.shortcut[0]), st, 0, training)
             scs, shs, mus, ivs = _BN.forward(m, ss, blk.shortcut[1], cnt, training, group)
-            out = m.bn_apply(y2, sc2, sh2, ys, scs, shs, 1, True)
+            om = _omask(y2, training)
+            out = m.bn_apply(y2, sc2, sh2, ys, scs, shs, 1, True, mask_out=om)
         else:
-            out = m.bn_apply(y2, sc2, sh2, x, None, None, 2, True)
+            om = _omask(y2, training)
+            out = m.bn_apply(y2, sc2, sh2, x, None, None, 2, True, mask_out=om)
         if training:
-            ctx.save_for_backward(x, y1, None if f1 is not None else a1, y2, ys, out, mu1, iv1, mu2, iv2, mus, ivs,
+            ctx.save_for_backward(x, y1, None if f1 is not None else a1, y2, ys, om, mu1, iv1, mu2, iv2, mus, ivs,
                                   sc1, sh1)
             ctx.blk, ctx.wc, ctx.group, ctx.params, ctx.cnt = blk, wc, group, params, cnt
         return out
