@@ -105,7 +105,8 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
 }
 
 torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                         int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend) {
+                         int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
+                         c10::optional<torch::Tensor> addend_mask) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
   TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
@@ -133,9 +134,17 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
     TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
     add = addend->data_ptr();
   }
+  const void* amask = nullptr;
+  if (addend_mask.has_value()) {
+    TORCH_CHECK(add != nullptr, "addend_mask needs an addend");
+    TORCH_CHECK(addend_mask->is_cuda() && addend_mask->scalar_type() == at::kByte && addend_mask->is_contiguous() &&
+                    addend_mask->numel() * 8 == dx.numel(),
+                "addend_mask: uint8 [numel/8]");
+    amask = addend_mask->data_ptr();
+  }
   if (stride == 1) {
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                      cur_stream()),
+                                      cur_stream(), amask),
               "conv_dgrad");
     return dx;
   }
@@ -150,7 +159,7 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
       else
         wc = wt;   // no taps: the kernel writes zeros and never reads B
       check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                        cur_stream()),
+                                        cur_stream(), amask),
                 "conv_dgrad(class)");
     }
   return dx;
@@ -717,20 +726,23 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
     auto c = bn_bwd_reduce_coef(dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
                                 c10::nullopt, cnt_last, G(lastbn, 0), S(lastbn, 3), c10::nullopt, c10::nullopt,
                                 G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt);
-    auto r = bn_bwd_apply(dout, out, ylast, c[0], c10::nullopt, c10::nullopt, true, c10::nullopt, c10::nullopt);
+    // identity shortcut: its gradient dz = dout·[out > 0] is never materialised when the ReLU
+    // bitmask is available — the last dgrad epilogue adds dout under the mask
+    const bool bitmask = out.scalar_type() == at::kByte;
+    auto r = bn_bwd_apply(dout, out, ylast, c[0], c10::nullopt, c10::nullopt, !bitmask, c10::nullopt, c10::nullopt);
     dylast = r[0];
-    dz = r[2];
+    dz = bitmask ? torch::Tensor() : r[2];
   }
   torch::Tensor dy1;
   if (bottleneck) {
     side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
-    auto da2 = conv_dgrad(dylast, wt[2], y2.size(1), y2.size(2), 1, 0, -1, c10::nullopt, c10::nullopt);
+    auto da2 = conv_dgrad(dylast, wt[2], y2.size(1), y2.size(2), 1, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt);
     auto c2 = bn_bwd_reduce_coef(da2, c10::nullopt, y2, S(1, 2), c10::nullopt, c10::nullopt, S(1, 0), S(1, 1),
                                  cnt_last, G(1, 0), S(1, 3), c10::nullopt, c10::nullopt, G(1, 1), G(1, 2),
                                  c10::nullopt, c10::nullopt);
     auto dy2 = bn_bwd_apply(da2, c10::nullopt, y2, c2[0], c10::nullopt, c10::nullopt, false, S(1, 0), S(1, 1))[0];
     side_wgrad(dy2, a1, 3, 3, stride, 1, dw[1], side);
-    auto da1 = conv_dgrad(dy2, wt[1], H, W, stride, 1, -1, c10::nullopt, c10::nullopt);
+    auto da1 = conv_dgrad(dy2, wt[1], H, W, stride, 1, -1, c10::nullopt, c10::nullopt, c10::nullopt);
     auto c1 = bn_bwd_reduce_coef(da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
                                  cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
                                  c10::nullopt);
@@ -738,7 +750,7 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
     side_wgrad(dy1, x, 1, 1, 1, 0, dw[0], side);
   } else {
     side_wgrad(dylast, a1, 3, 3, 1, 1, dw[1], side);
-    auto da1 = conv_dgrad(dylast, wt[1], y1.size(1), y1.size(2), 1, 1, -1, c10::nullopt, c10::nullopt);
+    auto da1 = conv_dgrad(dylast, wt[1], y1.size(1), y1.size(2), 1, 1, -1, c10::nullopt, c10::nullopt, c10::nullopt);
     auto c1 = bn_bwd_reduce_coef(da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
                                  cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
                                  c10::nullopt);
@@ -749,10 +761,12 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
   torch::Tensor dx;
   if (proj) {
     side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);
-    dx = conv_dgrad(dys, wt[nconv], H, W, stride, 0, -1, c10::nullopt, c10::nullopt);
-    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, dx, dx);
+    dx = conv_dgrad(dys, wt[nconv], H, W, stride, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt);
+    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, dx, dx, c10::nullopt);
+  } else if (dz.defined()) {
+    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, c10::nullopt, dz, c10::nullopt);
   } else {
-    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, c10::nullopt, dz);
+    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, c10::nullopt, dout, out);
   }
   return dx;
 }
@@ -767,7 +781,7 @@ void register_conv_bn(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv data gradient (strided: sub-pixel classes)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("addend") = pybind11::none());
+        pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none());
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K slab)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("splits") = 0, pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),

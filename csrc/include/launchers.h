@@ -37,7 +37,7 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
-                                   const void* addend, int cfg, hipStream_t s);
+                                   const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
 // partial: fp32 [splits][K][R*S*C] workspace (unused when splits == 1 and !accumulate)
 hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,

@@ -36,6 +36,9 @@ namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int BK = 64;
+#ifndef SDX_FRAG_PIN
+#define SDX_FRAG_PIN 0
+#endif
 
 struct IgemmParams {
   ConvGeom g;
@@ -51,6 +54,8 @@ struct IgemmParams {
   // diagnostic ablation (SDX_IGEMM_ABLATE bits, timing only — results are wrong):
   // 1 skip LDS stores, 2 skip global loads, 4 skip MFMAs
   int ablate;
+  // DGRAD addend ReLU bitmask (uint8, bit per element): addend element used iff its bit is set
+  const uint8_t* addend_mask;
   // operand sizes in elements (bounds checks of the checked build)
   long a_elems, b_elems;
   int M, Ncol, Kdim;
@@ -503,30 +508,38 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     return f;
   };
 
+  constexpr bool FRAG_PIN = SDX_FRAG_PIN;
   auto compute = [&](int buf) {
     if (p.ablate & 4) return;
     const unsigned char* sa = smem + buf * T::STAGE;
     const unsigned char* sb = sa + T::A_BYTES;
+    // all fragments of both 32-deep k-steps are requested up front (distinct registers),
+    // so the MFMAs of step 0 overlap the LDS latency of step 1 and no lgkmcnt(0) drain
+    // sits between MFMA groups (the compiler otherwise recycles two A-fragment registers
+    // and stalls on each refill)
+    bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        if (T::A_KIN) af[i] = frag_kin(sa, wm * WTM + 16 * i + c, u);
-        else af[i] = frag_kout(sa, wm * WTM + 16 * i, u, std::integral_constant<int, BM>{});
-      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if (T::B_KIN) bfr[j] = frag_kin(sb, wn * WTN + 16 * j + c, u);
-        else bfr[j] = frag_kout(sb, wn * WTN + 16 * j, u, std::integral_constant<int, BN>{});
+        if (T::B_KIN) bfr[u][j] = frag_kin(sb, wn * WTN + 16 * j + c, u);
+        else bfr[u][j] = frag_kout(sb, wn * WTN + 16 * j, u, std::integral_constant<int, BN>{});
       }
-      // D = Bᵀ·Aᵀ: accumulator column = output row (lane c), rows = output columns (4h + r)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (T::A_KIN) af[u][i] = frag_kin(sa, wm * WTM + 16 * i + c, u);
+        else af[u][i] = frag_kout(sa, wm * WTM + 16 * i, u, std::integral_constant<int, BM>{});
+      }
+    }
+    if (FRAG_PIN) __builtin_amdgcn_sched_barrier(0);   // keep all fragment reads ahead of the MFMAs
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
+          // D = Bᵀ·Aᵀ: accumulator column = output row (lane c), rows = output columns (4h + r)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[u][j], af[u][i], acc[i][j], 0, 0, 0);
   };
 
   // K loop: two LDS buffers, one barrier per K-tile. DEPTH 1: the loads of tile k+1 are in
@@ -641,7 +654,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         uint4 v = make_uint4(lo.x, lo.y, hi.x, hi.y);
         if (MODE == MODE_DGRAD && p.addend != nullptr) {
           // fused residual-gradient accumulation: out = dgrad + addend (may alias out)
-          const uint4 a = *reinterpret_cast<const uint4*>(p.addend + (size_t)orow * p.Ncol + col);
+          uint4 a = *reinterpret_cast<const uint4*>(p.addend + (size_t)orow * p.Ncol + col);
+          if (p.addend_mask != nullptr) {
+            // addend = dout·[out > 0] from the block output's 1-bit ReLU mask (no dz tensor)
+            const uint32_t mb = p.addend_mask[((size_t)orow * p.Ncol + col) >> 3];
+            uint32_t* aw2 = reinterpret_cast<uint32_t*>(&a);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t keep = ((mb >> (2 * q)) & 1u ? 0x0000ffffu : 0u) | ((mb >> (2 * q + 1)) & 1u ? 0xffff0000u : 0u);
+              aw2[q] &= keep;
+            }
+          }
           const uint32_t* vw = reinterpret_cast<const uint32_t*>(&v);
           const uint32_t* aw = reinterpret_cast<const uint32_t*>(&a);
           uint32_t r[4];
@@ -840,8 +863,9 @@ void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* 
 }
 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
-                                   const void* addend, int cfg, hipStream_t s) {
+                                   const void* addend, int cfg, hipStream_t s, const void* addend_mask) {
   IgemmParams p{};
+  p.addend_mask = (const uint8_t*)addend_mask;
   p.g = g;
   p.a = (const uint16_t*)dy;
   p.b = (const uint16_t*)wt_cls;

@@ -172,7 +172,8 @@ class _Bottleneck(torch.autograd.Function):
             dy3, dys, _ = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group, ys, mus, ivs, blk.shortcut[1])
             dz = None
         else:
-            dy3, _, dz = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group, want_dz=True)
+            # identity shortcut: dz = dout·mask is folded into the last dgrad epilogue
+            dy3, _, _ = _bn_bwd(m, dout, out, y3, mu3, iv3, blk.bn3, cnt2, group)
         _wgrad(m, dy3, y2 if f2 else a2, blk.conv3, 1, 0, f2)
         da2 = m.conv_dgrad(dy3, wc.dgrad(blk.conv3), y2.shape[1], y2.shape[2], 1, 0)
         # ReLU mask recomputed from y (read anyway) instead of reading the activation
@@ -186,7 +187,7 @@ class _Bottleneck(torch.autograd.Function):
             dx = m.conv_dgrad(dys, wc.dgrad(blk.shortcut[0]), H, W, st, 0)
             dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, 1, 0, -1, dx, dx)
         else:
-            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, 1, 0, -1, None, dz)
+            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, 1, 0, -1, None, dout, out)
         sinks.notify(ctx.params)
         return (dx, None, None, None, None) + (None,) * len(ctx.params)
 
@@ -232,7 +233,7 @@ class _Basic(torch.autograd.Function):
             dy2, dys, _ = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group, ys, mus, ivs, blk.shortcut[1])
             dz = None
         else:
-            dy2, _, dz = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group, want_dz=True)
+            dy2, _, _ = _bn_bwd(m, dout, out, y2, mu2, iv2, blk.bn2, cnt, group)
         _wgrad(m, dy2, y1 if f1 else a1, blk.conv2, 1, 1, f1)
         da1 = m.conv_dgrad(dy2, wc.dgrad(blk.conv2), y1.shape[1], y1.shape[2], 1, 1)
         dy1, _, _ = _bn_bwd(m, da1, None, y1, mu1, iv1, blk.bn1, cnt, group, mask=(sc1, sh1))
@@ -242,7 +243,7 @@ class _Basic(torch.autograd.Function):
             dx = m.conv_dgrad(dys, wc.dgrad(blk.shortcut[0]), H, W, st, 0)
             dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, st, 1, -1, dx, dx)
         else:
-            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, st, 1, -1, None, dz)
+            dx = m.conv_dgrad(dy1, wc.dgrad(blk.conv1), H, W, st, 1, -1, None, dout, out)
         sinks.notify(ctx.params)
         return (dx, None, None, None, None) + (None,) * len(ctx.params)
 

@@ -146,3 +146,21 @@ def test_conv_bn_relu_prologue(gpu, shape, cfg):
     dw_ref = m.conv_wgrad(dy, a, R, R, st, pad, 0, cfg)
     dw = m.conv_wgrad(dy, yh, R, R, st, pad, 0, cfg, None, False, sc, sh)
     assert _rel(dw, dw_ref) < 1e-2
+
+
+def test_dgrad_masked_addend(gpu):
+    """conv_dgrad(addend=g, addend_mask=bits) == conv_dgrad + g·[bit] (fused identity-shortcut
+    gradient of a ReLU'd block output)."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(9)
+    N, H, W, C, K = 4, 8, 8, 64, 256
+    dy = torch.randn(N, H, W, K, device=gpu).bfloat16()
+    wt = (torch.randn(C, 1, 1, K, device=gpu) * 0.05).bfloat16()
+    g = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    bits = torch.randint(0, 256, (g.numel() // 8,), dtype=torch.uint8, device=gpu)
+    ref = m.conv_dgrad(dy, wt, H, W, 1, 0).float()
+    keep = ((bits.long().unsqueeze(1) >> torch.arange(8, device=gpu)) & 1).reshape(g.shape).float()
+    exp = ref + g.float() * keep
+    out = m.conv_dgrad(dy, wt, H, W, 1, 0, -1, None, g, bits)
+    assert _rel(out, exp) < 1e-2
