@@ -54,6 +54,8 @@ struct IgemmParams {
   // diagnostic ablation (SDX_IGEMM_ABLATE bits, timing only — results are wrong):
   // 1 skip LDS stores, 2 skip global loads, 4 skip MFMAs
   int ablate;
+  // log2(Q), log2(P*Q) when both are powers of two, else -1 (WGRAD pixel decode)
+  int lq, lpq;
   // DGRAD addend ReLU bitmask (uint8, bit per element): addend element used iff its bit is set
   const uint8_t* addend_mask;
   // operand sizes in elements (bounds checks of the checked build)
@@ -214,6 +216,21 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     kr = rs / tap_s;
     ks = rs - kr * tap_s;
   }
+  // output pixel index -> (image, row, col): shifts when P and Q are powers of two
+  // (every ResNet stage at 32x32 / 224x224-derived sizes), magic-number division otherwise
+  auto pix_decode = [&](int kk, int& n, int& pp, int& qq) {
+    if (p.lq >= 0) {
+      n = kk >> p.lpq;
+      const int rem = kk & ((1 << p.lpq) - 1);
+      pp = rem >> p.lq;
+      qq = rem & ((1 << p.lq) - 1);
+    } else {
+      n = (int)fdiv((unsigned)kk, p.div_pq);
+      const int rem = kk - n * g.P * g.Q;
+      pp = (int)fdiv((unsigned)rem, p.div_q);
+      qq = rem - pp * g.Q;
+    }
+  };
   // WGRAD: K-outer images. A: [BK pixels][BM couts], B: [BK pixels][BN (r,s,ci)].
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;  // chunks per row
   int wb_r = 0, wb_s = 0, wb_c = 0;
@@ -341,10 +358,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         if (is1x1) {
           off = kk * g.C + wb_c;
         } else {
-          const int n = (int)fdiv((unsigned)kk, p.div_pq);
-          const int rem = kk - n * g.P * g.Q;
-          const int pp = (int)fdiv((unsigned)rem, p.div_q);
-          const int qq = rem - pp * g.Q;
+          int n, pp, qq;
+          pix_decode(kk, n, pp, qq);
           const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
           ok = ok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
           off = ((n * g.H + yy) * g.W + xx) * g.C + wb_c;
@@ -384,10 +399,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         if (is1x1) {
           off = kk * g.C + gb_c[i];
         } else {
-          const int n = (int)fdiv((unsigned)kk, p.div_pq);
-          const int rem = kk - n * g.P * g.Q;
-          const int pp = (int)fdiv((unsigned)rem, p.div_q);
-          const int qq = rem - pp * g.Q;
+          int n, pp, qq;
+          pix_decode(kk, n, pp, qq);
           const int yy = pp * g.stride - g.pad + gb_r[i], xx = qq * g.stride - g.pad + gb_s[i];
           ok = ok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
           off = ((n * g.H + yy) * g.W + xx) * g.C + gb_c[i];
@@ -912,6 +925,14 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
   p.splits = (p.Kdim + per - 1) / per;
   p.div_pq = make_fastdiv((unsigned)(g.P * g.Q));
   p.div_q = make_fastdiv((unsigned)g.Q);
+  auto log2_exact = [](int v) {
+    int l = 0;
+    while ((1 << l) < v) ++l;
+    return (1 << l) == v ? l : -1;
+  };
+  p.lq = log2_exact(g.Q);
+  p.lpq = log2_exact(g.P * g.Q);
+  if (p.lq < 0 || p.lpq < 0) p.lq = p.lpq = -1;
   // a single split writes straight into dW (unless accumulating)
   const bool direct = p.splits == 1 && !accumulate;
   p.out = direct ? (void*)dw : (void*)partial;
