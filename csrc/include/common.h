@@ -46,8 +46,14 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// two fp32 -> packed bf16x2 (RNE) in ONE v_cvt_pk_bf16_f32 (two scalar conversions cost
+// 2 cvt + and + shift + or)
+typedef __bf16 sdx_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float sdx_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const sdx_f32x2 v = {lo, hi};
+  const sdx_bf16x2 r = __builtin_convertvector(v, sdx_bf16x2);
+  return __builtin_bit_cast(uint32_t, r);
 }
 
 // Sum over the 16 lanes of each DPP row (lanes 16r..16r+15), result in every lane of the

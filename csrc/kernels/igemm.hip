@@ -36,6 +36,9 @@ namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int BK = 64;
+#ifndef SDX_FAST_TAPS
+#define SDX_FAST_TAPS 0
+#endif
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
@@ -215,6 +218,36 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     const int rs = k / cdim;
     kr = rs / tap_s;
     ks = rs - kr * tap_s;
+  }
+  // Uniform-tap fast path of the LDS-DMA loader: when the channel dim is a multiple of BK
+  // every K-tile lies inside one filter tap, so the tap (and the channel base) is
+  // wave-uniform: per-row validity over all taps is precomputed as a bitmask and a chunk
+  // address is row base + uniform tap offset + lane constant (no per-chunk multiplies).
+  const int taps = (MODE == MODE_FWD) ? g.R * g.S : p.nr * p.ns;
+  const bool fast_taps = SDX_FAST_TAPS && GL && MODE != MODE_WGRAD && (cdim % BK) == 0 && taps <= 32;
+  constexpr int FCH = (GL && MODE != MODE_WGRAD) ? T::A_CH : 1;
+  unsigned vmask[FCH];
+  int rbase[FCH];
+  int u_c0 = 0, u_ks = 0, u_kr = 0;
+  if (fast_taps) {
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      unsigned mbits = 0;
+      const bool row_ok = a_y[i] > -(1 << 27);
+      const int nrr = (MODE == MODE_FWD) ? g.R : p.nr;
+      for (int r = 0; r < nrr; ++r)
+        for (int q = 0; q < tap_s; ++q) {
+          bool v;
+          if (MODE == MODE_FWD)
+            v = (unsigned)(a_y[i] + r) < (unsigned)g.H && (unsigned)(a_x[i] + q) < (unsigned)g.W;
+          else
+            v = (unsigned)(a_y[i] - r) < (unsigned)g.P && (unsigned)(a_x[i] - q) < (unsigned)g.Q;
+          if (row_ok && v) mbits |= 1u << (r * tap_s + q);
+        }
+      vmask[i] = mbits;
+      rbase[i] = !row_ok ? 0
+                 : (MODE == MODE_FWD ? a_base[i] : a_base[i] + (a_y[i] * g.Q + a_x[i]) * g.K);
+    }
   }
   // output pixel index -> (image, row, col): shifts when P and Q are powers of two
   // (every ResNet stage at 32x32 / 224x224-derived sizes), magic-number division otherwise
@@ -415,6 +448,36 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     }
     const int k = k0 + kin_ch * 8;
     const bool kok = k < k_end;
+    if (fast_taps) {
+      const int tap = u_kr * tap_s + u_ks;
+      const int toff = (MODE == MODE_FWD) ? (u_kr * g.W + u_ks) * g.C + u_c0 : -(u_kr * g.Q + u_ks) * g.K + u_c0;
+      const int lane_c = kin_ch * 8;
+#pragma unroll
+      for (int i = 0; i < FCH; ++i) {
+        const bool ok = kok && ((vmask[i] >> tap) & 1u);
+        const int off = rbase[i] + toff + lane_c;
+        SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
+        const uint16_t* src = ok ? p.a + off : g_zero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
+                                         16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < T::B_CH; ++i) {
+        const bool ok = kok && b_off[i] >= 0;
+        SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
+        const uint16_t* src = ok ? p.b + b_off[i] + k : g_zero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
+                                         16, 0, 0);
+      }
+      u_c0 += BK;
+      if (u_c0 == cdim) {
+        u_c0 = 0;
+        if (++u_ks == tap_s) { u_ks = 0; ++u_kr; }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
       bool ok;
