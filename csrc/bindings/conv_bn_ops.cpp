@@ -67,6 +67,11 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim = 0, bool fill = false) {
     const double sc = padded * (long_k ? pen_long[c] : pen_short[c]) * f;
     if (sc < best_s) { best_s = sc; best = c; }
   }
+  // fwd/dgrad: the 8-wave 128x128 tile (cfg 4, 2x4 waves of 64x32) beats the 4-wave one by
+  // 3-12% on every ResNet-50 shape with a reduction of >= 128 (more waves hide the LDS-DMA
+  // and epilogue latency); on the K=64 layer-1 GEMMs its longer prologue costs more than it
+  // hides. wgrad keeps the 4-wave tiles (its split-K slabs are short). profiles/conv_cfg4_r1.txt
+  if (fill && best == 0 && Kdim >= 128) best = 4;
   return best;
 }
 

@@ -120,7 +120,7 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int NT>
 struct Tile {
   static constexpr bool A_KIN = MODE != MODE_WGRAD;
   static constexpr bool B_KIN = MODE != MODE_WGRAD;
@@ -128,8 +128,8 @@ struct Tile {
   static constexpr int B_BYTES = BN * BK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   // chunks (16 B) per thread
-  static constexpr int A_CH = BM * BK / 8 / 256;
-  static constexpr int B_CH = BN * BK / 8 / 256;
+  static constexpr int A_CH = BM * BK / 8 / NT;
+  static constexpr int B_CH = BN * BK / 8 / NT;
 };
 
 // DEPTH: 1 / 2 = register-staged operands, 1 or 2 K-tiles of prefetch; 3 = LDS-DMA
@@ -137,11 +137,13 @@ struct Tile {
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
-__global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
-  using T = Tile<MODE, BM, BN>;
+__global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
+  constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
+  using T = Tile<MODE, BM, BN, NT>;
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves");
+  static_assert(T::A_CH >= 1 && T::B_CH >= 1, "tile too small for the thread count");
   constexpr int LDS = 2 * T::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
@@ -166,14 +168,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
 
   // ---- per-thread loader state (32-bit address math: tensors < 2^31 elements) ----
   // K-inner operands. Register staging: thread owns chunk column ch = tid % 8 and rows
-  // tid/8 + 32*i. LDS-DMA: instruction i of wave w fills rows 8*(w*CH + i) .. +7 (1 KiB),
+  // tid/8 + (NT/8)*i. LDS-DMA: instruction i of wave w fills rows 8*(w*CH + i) .. +7 (1 KiB),
   // lane L row +L/8 at physical chunk L%8, i.e. logical chunk (L&7)^(L>>3).
   constexpr bool GL = DEPTH == 3;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
   const int kin_ch = GL ? ((lane & 7) ^ ((lane >> 3) & 7)) : (tid & 7);
   const int kin_row0 = tid >> 3;
-  auto a_row = [&](int i) { return GL ? 8 * (wvu * T::A_CH + i) + (lane >> 3) : kin_row0 + 32 * i; };
-  auto b_row = [&](int i) { return GL ? 8 * (wvu * T::B_CH + i) + (lane >> 3) : kin_row0 + 32 * i; };
+  auto a_row = [&](int i) { return GL ? 8 * (wvu * T::A_CH + i) + (lane >> 3) : kin_row0 + (NT / 8) * i; };
+  auto b_row = [&](int i) { return GL ? 8 * (wvu * T::B_CH + i) + (lane >> 3) : kin_row0 + (NT / 8) * i; };
   const bool is1x1 = (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
   // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
   // tap; DGRAD: dy coordinate of tap (r0, s0))
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
       // WGRAD A: dy rows (pixels) x BM couts
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i) {
-        const int e = tid + 256 * i;
+        const int e = tid + NT * i;
         const int row = e / A_CPR, ch = e % A_CPR;
         const int kk = k0 + row, co = m0 + ch * 8;
         SDX_DCHECK(!(kk < k_end && co < p.M) || (long)kk * g.K + co + 8 <= p.a_elems);
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
       if (wb_bn) ld_mask = 0;
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        const int e = tid + 256 * i;
+        const int e = tid + NT * i;
         const int row = e / B_CPR;
         const int kk = k0 + row;
         bool ok = wb_ok && kk < k_end;
@@ -540,19 +542,19 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
     if (MODE != MODE_WGRAD) {
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i)
-        *reinterpret_cast<uint4*>(sa + kin_off(kin_row0 + 32 * i, kin_ch)) = ra[i];
+        *reinterpret_cast<uint4*>(sa + kin_off(kin_row0 + (NT / 8) * i, kin_ch)) = ra[i];
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i)
-        *reinterpret_cast<uint4*>(sb + kin_off(kin_row0 + 32 * i, kin_ch)) = rb[i];
+        *reinterpret_cast<uint4*>(sb + kin_off(kin_row0 + (NT / 8) * i, kin_ch)) = rb[i];
     } else {
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i) {
-        const int e = tid + 256 * i;
+        const int e = tid + NT * i;
         *reinterpret_cast<uint4*>(sa + kout_off<BM>(e / A_CPR, e % A_CPR)) = ra[i];
       }
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        const int e = tid + 256 * i;
+        const int e = tid + NT * i;
         *reinterpret_cast<uint4*>(sb + kout_off<BN>(e / B_CPR, e % B_CPR)) = rb[i];
       }
     }
@@ -713,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
   {
     uint16_t* out = reinterpret_cast<uint16_t*>(p.out);
     constexpr int CPR = BN / 8;
-    for (int e = tid; e < BM * CPR; e += 256) {
+    for (int e = tid; e < BM * CPR; e += NT) {
       const int row = e / CPR, ch = e % CPR;
       const int m = m0 + row, col = n0 + ch * 8;
       if (m < p.M && col < p.Ncol) {
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmParams p) {
         }
     }
     __syncthreads();
-    for (int e = tid; e < 2 * BN; e += 256) {
+    for (int e = tid; e < 2 * BN; e += NT) {
       const int which = e / BN, col = e % BN;
       float s = 0.f;
 #pragma unroll
@@ -876,24 +878,26 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
     // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
     // (SDX_IGEMM_GLDS=2 enables it there too)
     if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 3>), dim3(grid), dim3(256), 0, s, p);
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 3>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
   }
   if constexpr (kDepth2) {
     if (igemm_depth() == 2) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2>), dim3(grid), dim3(256), 0, s, p);
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
   }
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 1>), dim3(grid), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 1>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
 
-// tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32)
+// tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
+// 4 128x128 with 8 waves (2x4 of 64x32: twice the waves per SIMD for latency hiding),
+// 5 256x128 with 8 waves (4x2 of 64x64, 96 KiB LDS: one block per CU)
 template <int MODE>
 hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
   switch (cfg) {
@@ -901,14 +905,22 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
     case 1: return launch_cfg<MODE, 256, 64, 4, 1>(p, s);
     case 2: return launch_cfg<MODE, 64, 256, 1, 4>(p, s);
     case 3: return launch_cfg<MODE, 64, 64, 2, 2>(p, s);
+    case 4: return launch_cfg<MODE, 128, 128, 2, 4>(p, s);
+    case 5: return launch_cfg<MODE, 256, 128, 4, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 }  // namespace
 
-int igemm_tile_m(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 256 : 64; }
-int igemm_tile_n(int cfg) { return cfg == 0 ? 128 : cfg == 1 ? 64 : cfg == 2 ? 256 : 64; }
+int igemm_tile_m(int cfg) {
+  static const int m[6] = {128, 256, 64, 64, 128, 256};
+  return m[cfg];
+}
+int igemm_tile_n(int cfg) {
+  static const int n[6] = {128, 64, 256, 64, 128, 128};
+  return n[cfg];
+}
 
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s, const float* in_scale, const float* in_shift) {
