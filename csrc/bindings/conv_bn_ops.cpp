@@ -582,18 +582,30 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Te
 // Native residual-block executor: the whole forward / backward kernel sequence of a
 // Bottleneck or BasicBlock (reference math: networks/resnet_big.py:7-67) in ONE host
 // call, so the per-kernel Python + binding overhead (≈15-25 µs per launch, measured)
-// leaves the training step. Single-process BN statistics only (SyncBN keeps the Python
-// path, which interleaves the cross-rank all-reduces). Weight gradients run on the caller's
-// side stream (fork/join by events, tensors recorded on that stream for the allocator).
+// leaves the training step. SyncBN statistics go through a native small communicator
+// (comm_ops.cpp: a dedicated RCCL communicator or a one-shot xGMI arena) called in place
+// on the compute stream — no Python or c10d work queue between a BN's reduction and its
+// finalize. Weight gradients run on the caller's side stream (fork/join by events,
+// tensors recorded on that stream for the allocator).
 // =====================================================================================
 
 struct BnState {          // per-BN forward results kept for backward
   torch::Tensor sc, sh, mu, iv;
 };
 
+// comm: small-communicator handle (comm_ops.cpp); 0 = this process's statistics only.
+// With a communicator, the per-channel (Σy, Σy²) are summed over its ranks (fp64, in place,
+// on the compute stream) between the reduction and the finalize — SyncBN semantics.
 BnState bn_forward(const torch::Tensor& slab, double count, const torch::Tensor& g, const torch::Tensor& b,
-                   const torch::Tensor& rm, const torch::Tensor& rv, double eps, double mom, bool training) {
+                   const torch::Tensor& rm, const torch::Tensor& rv, double eps, double mom, bool training,
+                   int64_t comm) {
   if (training) {
+    if (comm != 0 && small_comm_world(comm) > 1) {
+      auto sums = bn_stats_reduce(slab);
+      small_all_reduce_(comm, sums);
+      auto r = bn_finalize(sums, count * small_comm_world(comm), g, b, eps, mom, true, rm, rv);
+      return {r[0], r[1], r[2], r[3]};
+    }
     auto r = bn_stats_finalize(slab, count, g, b, eps, mom, true, rm, rv);
     return {r[0], r[1], r[2], r[3]};
   }
@@ -602,6 +614,21 @@ BnState bn_forward(const torch::Tensor& slab, double count, const torch::Tensor&
 }
 
 double rows_of(const torch::Tensor& y) { return (double)(y.numel() / y.size(3)); }
+
+// bn_bwd_reduce_coef, or (communicator of >1 ranks) reduce -> in-place all-reduce of the
+// [Σdz, Σdz·y(, Σdz·y_b)] sums -> coefficients, with count scaled to the global row count
+std::vector<torch::Tensor> bn_bwd_sync(int64_t comm, torch::Tensor dout, OptT outv, torch::Tensor ya,
+                                       torch::Tensor ma, OptT yb, OptT mb, OptT msc, OptT msh, double count,
+                                       OptT g_a, torch::Tensor inv_a, OptT g_b, OptT inv_b, OptT sink_ga,
+                                       OptT sink_ba, OptT sink_gb, OptT sink_bb) {
+  if (comm == 0 || small_comm_world(comm) == 1)
+    return bn_bwd_reduce_coef(dout, outv, ya, ma, yb, mb, msc, msh, count, g_a, inv_a, g_b, inv_b, sink_ga, sink_ba,
+                              sink_gb, sink_bb);
+  auto sums = bn_bwd_reduce(dout, outv, ya, ma, yb, mb, msc, msh);
+  small_all_reduce_(comm, sums);
+  return bn_bwd_coef(sums, count * small_comm_world(comm), g_a, ma, inv_a, g_b, mb, inv_b, sink_ga, sink_ba, sink_gb,
+                     sink_bb);
+}
 
 // event pool for side-stream fork points
 hipEvent_t next_event() {
@@ -642,7 +669,7 @@ void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int6
 //          then sc, sh, mu, iv per BN]
 std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor> w, std::vector<torch::Tensor> bn,
                                      int64_t stride, bool bottleneck, bool proj, bool training, double eps,
-                                     double momentum) {
+                                     double momentum, int64_t comm) {
   const int nconv = bottleneck ? 3 : 2;
   TORCH_CHECK((int)w.size() == nconv + (proj ? 1 : 0), "block_fwd: weight count");
   TORCH_CHECK(bn.size() == w.size() * 4, "block_fwd: 4 BN tensors per conv");
@@ -652,18 +679,18 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
   auto c1 = conv_fwd(x, w[0], s1, p1, training, -1, c10::nullopt, c10::nullopt);
   const double cnt1 = rows_of(c1[0]);
-  st.push_back(bn_forward(c1[1], cnt1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training));
+  st.push_back(bn_forward(c1[1], cnt1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training, comm));
   auto a1 = bn_apply(c1[0], st[0].sc, st[0].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
   const int64_t s2 = bottleneck ? stride : 1;
   auto c2 = conv_fwd(a1, w[1], s2, 1, training, -1, c10::nullopt, c10::nullopt);
   const double cnt2 = rows_of(c2[0]);
-  st.push_back(bn_forward(c2[1], cnt2, B(1, 0), B(1, 1), B(1, 2), B(1, 3), eps, momentum, training));
+  st.push_back(bn_forward(c2[1], cnt2, B(1, 0), B(1, 1), B(1, 2), B(1, 3), eps, momentum, training, comm));
   torch::Tensor last = c2[0], a2;
   int lastbn = 1;
   if (bottleneck) {
     a2 = bn_apply(c2[0], st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
     auto c3 = conv_fwd(a2, w[2], 1, 0, training, -1, c10::nullopt, c10::nullopt);
-    st.push_back(bn_forward(c3[1], cnt2, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training));
+    st.push_back(bn_forward(c3[1], cnt2, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm));
     last = c3[0];
     lastbn = 2;
   }
@@ -675,7 +702,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   if (proj) {
     auto cs = conv_fwd(x, w[nconv], stride, 0, training, -1, c10::nullopt, c10::nullopt);
     st.push_back(bn_forward(cs[1], cnt2, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
-                            training));
+                            training, comm));
     ys = cs[0];
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true, om);
   } else {
@@ -705,7 +732,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
 // bng: [gamma, dgamma_sink, dbeta_sink] per BN. Returns dx.
 torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, std::vector<torch::Tensor> bnst,
                         std::vector<torch::Tensor> wt, std::vector<torch::Tensor> dw, std::vector<torch::Tensor> bng,
-                        int64_t stride, bool bottleneck, bool proj, int64_t side) {
+                        int64_t stride, bool bottleneck, bool proj, int64_t side, int64_t comm) {
   const int nconv = bottleneck ? 3 : 2;
   const int nbn = nconv + (proj ? 1 : 0);
   TORCH_CHECK((int)wt.size() == nbn && (int)dw.size() == nbn && (int)bng.size() == 3 * nbn &&
@@ -721,14 +748,14 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
   const double cnt_last = rows_of(ylast), cnt1 = rows_of(y1);
   torch::Tensor dylast, dys, dz;
   if (proj) {
-    auto c = bn_bwd_reduce_coef(dout, out, ylast, S(lastbn, 2), ys, S(nconv, 2), c10::nullopt, c10::nullopt,
+    auto c = bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), ys, S(nconv, 2), c10::nullopt, c10::nullopt,
                                 cnt_last, G(lastbn, 0), S(lastbn, 3), G(nconv, 0), S(nconv, 3), G(lastbn, 1),
                                 G(lastbn, 2), G(nconv, 1), G(nconv, 2));
     auto r = bn_bwd_apply(dout, out, ylast, c[0], ys, c[1], false, c10::nullopt, c10::nullopt);
     dylast = r[0];
     dys = r[1];
   } else {
-    auto c = bn_bwd_reduce_coef(dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
+    auto c = bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
                                 c10::nullopt, cnt_last, G(lastbn, 0), S(lastbn, 3), c10::nullopt, c10::nullopt,
                                 G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt);
     // identity shortcut: its gradient dz = dout·[out > 0] is never materialised when the ReLU
@@ -742,13 +769,13 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
   if (bottleneck) {
     side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
     auto da2 = conv_dgrad(dylast, wt[2], y2.size(1), y2.size(2), 1, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    auto c2 = bn_bwd_reduce_coef(da2, c10::nullopt, y2, S(1, 2), c10::nullopt, c10::nullopt, S(1, 0), S(1, 1),
+    auto c2 = bn_bwd_sync(comm, da2, c10::nullopt, y2, S(1, 2), c10::nullopt, c10::nullopt, S(1, 0), S(1, 1),
                                  cnt_last, G(1, 0), S(1, 3), c10::nullopt, c10::nullopt, G(1, 1), G(1, 2),
                                  c10::nullopt, c10::nullopt);
     auto dy2 = bn_bwd_apply(da2, c10::nullopt, y2, c2[0], c10::nullopt, c10::nullopt, false, S(1, 0), S(1, 1))[0];
     side_wgrad(dy2, a1, 3, 3, stride, 1, dw[1], side);
     auto da1 = conv_dgrad(dy2, wt[1], H, W, stride, 1, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    auto c1 = bn_bwd_reduce_coef(da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
+    auto c1 = bn_bwd_sync(comm, da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
                                  cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
                                  c10::nullopt);
     dy1 = bn_bwd_apply(da1, c10::nullopt, y1, c1[0], c10::nullopt, c10::nullopt, false, S(0, 0), S(0, 1))[0];
@@ -756,7 +783,7 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
   } else {
     side_wgrad(dylast, a1, 3, 3, 1, 1, dw[1], side);
     auto da1 = conv_dgrad(dylast, wt[1], y1.size(1), y1.size(2), 1, 1, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    auto c1 = bn_bwd_reduce_coef(da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
+    auto c1 = bn_bwd_sync(comm, da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
                                  cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
                                  c10::nullopt);
     dy1 = bn_bwd_apply(da1, c10::nullopt, y1, c1[0], c10::nullopt, c10::nullopt, false, S(0, 0), S(0, 1))[0];
@@ -816,8 +843,14 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("inv_b") = pybind11::none(), pybind11::arg("sink_ga") = pybind11::none(),
         pybind11::arg("sink_ba") = pybind11::none(), pybind11::arg("sink_gb") = pybind11::none(),
         pybind11::arg("sink_bb") = pybind11::none());
-  m.def("block_fwd", &block_fwd, "native residual-block forward (whole kernel sequence, single-process BN)");
-  m.def("block_bwd", &block_bwd, "native residual-block backward (dgrad chain + side-stream wgrads)");
+  m.def("block_fwd", &block_fwd, "native residual-block forward (whole kernel sequence; comm: SyncBN handle or 0)",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bn"), pybind11::arg("stride"),
+        pybind11::arg("bottleneck"), pybind11::arg("proj"), pybind11::arg("training"), pybind11::arg("eps"),
+        pybind11::arg("momentum"), pybind11::arg("comm") = 0);
+  m.def("block_bwd", &block_bwd, "native residual-block backward (dgrad chain + side-stream wgrads)",
+        pybind11::arg("dout"), pybind11::arg("saved"), pybind11::arg("bnst"), pybind11::arg("wt"),
+        pybind11::arg("dw"), pybind11::arg("bng"), pybind11::arg("stride"), pybind11::arg("bottleneck"),
+        pybind11::arg("proj"), pybind11::arg("side"), pybind11::arg("comm") = 0);
   m.def("bn_bwd_apply", &bn_bwd_apply, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
         pybind11::arg("ca"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("cb") = pybind11::none(),
         pybind11::arg("want_dz") = false, pybind11::arg("msc") = pybind11::none(),

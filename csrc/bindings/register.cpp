@@ -9,6 +9,7 @@ void register_optim(pybind11::module& m);
 void register_pool(pybind11::module& m);
 void register_wprep(pybind11::module& m);
 void register_xgmi(pybind11::module& m);
+void register_comm(pybind11::module& m);
 
 void register_ops(pybind11::module& m) {
   register_supcon(m);
@@ -18,5 +19,6 @@ void register_ops(pybind11::module& m) {
   register_pool(m);
   register_wprep(m);
   register_xgmi(m);
+  register_comm(m);
 }
 }  // namespace sdx_bind

@@ -149,6 +149,10 @@ torch::Tensor xgmi_emulate(torch::Tensor in, int64_t iters) {
 
 }  // namespace
 
+// for comm_ops.cpp (small-communicator wrapper of an arena)
+torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x) { return xgmi_allreduce(id, x); }
+int64_t xgmi_world(int64_t id) { return get(id).world; }
+
 void register_xgmi(pybind11::module& m) {
   m.def("xgmi_create", &xgmi_create, "allocate this rank's IPC receive arena (uncached device memory)");
   m.def("xgmi_handle", &xgmi_handle, "64-byte IPC handle of this rank's arena");

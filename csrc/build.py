@@ -106,7 +106,7 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         libs = []
         for p in lib_torch:
             libs += [f"-L{p}", f"-Wl,-rpath,{p}"]
-        libs += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
+        libs += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]  # RCCL symbols resolve from torch's own librccl.so (a dependency of libtorch_hip)
         tmp = out_so + ".tmp"
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + libs
         if verbose:

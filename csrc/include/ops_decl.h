@@ -9,4 +9,8 @@ hipStream_t cur_stream();
 void check_hip(hipError_t e, const char* what);
 
 void register_ops(pybind11::module& m);
+
+// native small communicators (comm_ops.cpp): handle 0 = single process
+int small_comm_world(int64_t h);
+void small_all_reduce_(int64_t h, torch::Tensor& x);
 }  // namespace sdx_bind

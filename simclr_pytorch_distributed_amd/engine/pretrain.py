@@ -94,13 +94,7 @@ class PretrainEngine:
                 model = convert_sync_bn(model)
             else:
                 self.sync_group = dist.group.WORLD
-                if getattr(opt, "syncbn_comm", "rccl") == "xgmi":
-                    try:
-                        from ..parallel.xgmi import OneShotAllReduce
-                        comm.set_small_allreduce(None, OneShotAllReduce())
-                        logging.info("SyncBN statistics: one-shot xGMI all-reduce")
-                    except Exception as e:  # noqa: BLE001
-                        logging.warning(f"one-shot xGMI all-reduce unavailable ({e}); using RCCL")
+                self._setup_syncbn_comm(opt, dev)
         model = model.to(dev)
         if dev.type == "cuda":
             model = model.to(memory_format=torch.channels_last)
@@ -137,6 +131,31 @@ class PretrainEngine:
             self._resume(opt.resume)
 
     # ------------------------------------------------------------------------------
+    def _setup_syncbn_comm(self, opt, dev):
+        """SyncBN statistics transport for the native backend.
+
+        ``--syncbn_comm xgmi``: one-shot IPC arena (every rank stores its payload into
+        every peer, one flag round trip). ``rccl`` (default): a dedicated RCCL
+        communicator. Either is registered as a native handle, so the C++ block
+        executor all-reduces each BN's sums itself on the compute stream. gloo (CPU
+        tests, shared-GPU tests) keeps the Python collective path."""
+        want = getattr(opt, "syncbn_comm", "rccl")
+        if dev.type != "cuda":
+            return
+        if want == "xgmi":
+            try:
+                from ..parallel.xgmi import OneShotAllReduce
+                impl = OneShotAllReduce()
+                comm.set_small_allreduce(None, impl)
+                comm.set_native_small_comm(None, _ext.require().xgmi_small_comm(impl.id, comm.rank()))
+                logging.info("SyncBN statistics: one-shot xGMI all-reduce (native executor)")
+                return
+            except Exception as e:  # noqa: BLE001
+                logging.warning(f"one-shot xGMI all-reduce unavailable ({e}); using RCCL")
+        if comm.backend() == "nccl" and os.environ.get("SDX_NATIVE_SYNCBN", "1") != "0":
+            comm.set_native_small_comm(None, comm.create_rccl_small_comm(None))
+            logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
+
     def _resume(self, path):
         st = ckpt_mod.load_checkpoint(path)
         ckpt_mod.load_model_state(self.model, st["model"])

@@ -289,10 +289,12 @@ class _NativeBlock(torch.autograd.Function):
     ``block_fwd`` / ``block_bwd``): one host call per block and direction instead of
     ~12 / ~20 Python-level kernel calls. Same kernels and math as :class:`_Bottleneck` /
     :class:`_Basic` (materialised internal activations, ReLU masks from y in backward,
-    side-stream wgrads); used when BN statistics need no cross-rank all-reduce."""
+    side-stream wgrads). SyncBN: ``comm_h`` is a native small-communicator handle
+    (parallel/comm.py ``native_small_comm``); the executor all-reduces every BN's sums
+    itself, in place on the compute stream (0 = single-process statistics)."""
 
     @staticmethod
-    def forward(ctx, x, blk, wc, training, info, *params):
+    def forward(ctx, x, blk, wc, training, info, comm_h, *params):
         m = _ext.require()
         convs, bns, bottle, proj = info
         bn0 = bns[0]
@@ -300,14 +302,14 @@ class _NativeBlock(torch.autograd.Function):
         for bn in bns:
             bn_list += [bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var]
         r = m.block_fwd(x, [wc.fwd(cv) for cv in convs], bn_list, blk.stride, bottle, proj, training, bn0.eps,
-                        bn0.momentum)
+                        bn0.momentum, comm_h)
         out = r[0]
         if training:
             e = _empty(x)
             # r[7]: the block output's ReLU bitmask (1 bit/element) replaces `out` in backward
             saved = [x] + [t if t is not None else e for t in r[1:7]] + [r[7]]
             ctx.save_for_backward(*saved, *r[8:])
-            ctx.blk, ctx.wc, ctx.info, ctx.params = blk, wc, info, params
+            ctx.blk, ctx.wc, ctx.info, ctx.params, ctx.comm_h = blk, wc, info, params, comm_h
         return out
 
     @staticmethod
@@ -322,9 +324,9 @@ class _NativeBlock(torch.autograd.Function):
         from . import streams
         side = streams.side(dout.device).cuda_stream if streams.ENABLED else 0
         dx = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
-                         [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side)
+                         [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side, ctx.comm_h)
         sinks.notify(ctx.params)
-        return (dx, None, None, None, None) + (None,) * len(ctx.params)
+        return (dx, None, None, None, None, None) + (None,) * len(ctx.params)
 
 
 _EMPTY = {}
@@ -353,10 +355,16 @@ def _block_info(blk):
     return info
 
 
-def _use_native_exec(group, blk_info) -> bool:
+def _native_comm(group, blk_info) -> int:
+    """-1: Python block path; else the executor's SyncBN handle (0 = no SyncBN)."""
     bns = blk_info[1]
-    return (NATIVE_EXEC and group is None and not FUSE_PROLOGUE and bns[0].momentum is not None
-            and all(bn.affine and bn.track_running_stats for bn in bns))
+    if not (NATIVE_EXEC and not FUSE_PROLOGUE and bns[0].momentum is not None
+            and all(bn.affine and bn.track_running_stats for bn in bns)):
+        return -1
+    if group is None:
+        return 0
+    h = comm.native_small_comm(group)
+    return h if h else -1
 
 
 def block_params(mod) -> List[torch.nn.Parameter]:
@@ -366,15 +374,17 @@ def block_params(mod) -> List[torch.nn.Parameter]:
 
 def bottleneck(x, blk, wc, training: bool, group=None):
     info, params = _block_info(blk)
-    if _use_native_exec(group, info):
-        return _NativeBlock.apply(x, blk, wc, training, info, *params)
+    h = _native_comm(group, info)
+    if h >= 0:
+        return _NativeBlock.apply(x, blk, wc, training, info, h, *params)
     return _Bottleneck.apply(x, blk, wc, training, group, *params)
 
 
 def basic(x, blk, wc, training: bool, group=None):
     info, params = _block_info(blk)
-    if _use_native_exec(group, info):
-        return _NativeBlock.apply(x, blk, wc, training, info, *params)
+    h = _native_comm(group, info)
+    if h >= 0:
+        return _NativeBlock.apply(x, blk, wc, training, info, h, *params)
     return _Basic.apply(x, blk, wc, training, group, *params)
 
 

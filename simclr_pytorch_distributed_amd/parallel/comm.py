@@ -134,8 +134,59 @@ def set_small_allreduce(group, impl) -> None:
         _small[key] = impl
 
 
+_native = {}
+
+
+def _key(group):
+    return None if group is None or group is dist.group.WORLD else id(group)
+
+
+def set_native_small_comm(group, handle: int) -> None:
+    """Register a native small-communicator handle (csrc/bindings/comm_ops.cpp) for
+    ``group`` (None = WORLD). The native block executor then issues the SyncBN
+    all-reduces itself, in place on the compute stream; ``handle=0`` unregisters."""
+    if handle:
+        _native[_key(group)] = int(handle)
+    else:
+        _native.pop(_key(group), None)
+
+
+def native_small_comm(group) -> int:
+    """Handle for ``group`` (0 = none registered: use the Python collective path)."""
+    return _native.get(_key(group), 0)
+
+
+def create_rccl_small_comm(group=None) -> int:
+    """A dedicated RCCL communicator over ``group``'s ranks for SyncBN statistics.
+
+    Rank 0 draws an ``ncclUniqueId`` and broadcasts it through the process group
+    (the TCP/env rendezvous only carries this id); every rank then joins
+    with ``ncclCommInitRank``. Kept apart from torch's communicators, so the gradient
+    buckets on the reducer's comm stream never queue in front of a BN statistic.
+    """
+    from ..ops import _ext
+    m = _ext.require()
+    w, r = dist.get_world_size(group), dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    uid = m.rccl_unique_id() if r == 0 else torch.zeros(128, dtype=torch.uint8)
+    t = uid.to(dev) if backend() == "nccl" else uid
+    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    h = m.rccl_comm_init(t.cpu(), w, r)
+    # one warm-up all-reduce: fails loudly here rather than inside the first forward
+    probe = torch.ones(4, dtype=torch.float64, device=dev)
+    m.small_all_reduce_(h, probe)
+    if float(probe[0].item()) != float(w):
+        raise RuntimeError(f"RCCL small communicator self-check failed ({probe[0].item()} != {w})")
+    return h
+
+
 def small_all_reduce_(x: torch.Tensor, group=None) -> torch.Tensor:
     """In-place sum of a small, latency-bound tensor (SyncBN statistics)."""
+    h = _native.get(_key(group), 0)
+    if h and x.is_cuda and x.is_contiguous() and x.dtype == torch.float64:
+        from ..ops import _ext
+        _ext.require().small_all_reduce_(h, x)
+        return x
     impl = _small.get(id(group) if group is not None else None)
     if impl is None and group is dist.group.WORLD:
         impl = _small.get(None)

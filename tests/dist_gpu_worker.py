@@ -18,6 +18,7 @@ def main():
     from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
     from simclr_pytorch_distributed_amd.models.executor import to_nhwc_input
     from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.parallel import comm
     B = 16                                    # images per rank
     G = 32                                    # global images
     argv = ["--model", "resnet18", "--backend", "native", "--dist_backend", "gloo", "--synthetic",
@@ -25,6 +26,8 @@ def main():
             "--work_dir", out_dir, "--batch_size", str(G), "--ngpu", str(world)]
     if world > 1:
         argv.append("--syncBN")
+        if os.environ.get("SDX_TEST_SYNCBN_COMM"):
+            argv += ["--syncbn_comm", os.environ["SDX_TEST_SYNCBN_COMM"]]
     opt = parse_pretrain(argv, make_dirs=False)
     eng = PretrainEngine(opt, device=torch.device("cuda:0"))
     torch.manual_seed(123)
@@ -47,7 +50,7 @@ def main():
     torch.cuda.synchronize()
     bn = eng.model.encoder.layer1[0].bn1
     torch.save({"flat": eng.flat.flat.detach().cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
-                "loss": float(loss.detach()), "grad": grad.cpu(), "names": list(eng.flat.names),
+                "native_h": comm.native_small_comm(None), "loss": float(loss.detach()), "grad": grad.cpu(), "names": list(eng.flat.names),
                 "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"w{world}_r{rank}.pt"))
     if world > 1:
         import torch.distributed as dist

@@ -1,0 +1,95 @@
+"""Native small communicators (csrc/bindings/comm_ops.cpp) and the SyncBN path of the C++
+block executor (csrc/bindings/conv_bn_ops.cpp block_fwd / block_bwd with a comm handle).
+
+The box has one GPU, so multi-rank RCCL cannot run here: the RCCL kind is exercised
+with a 1-rank communicator (linking against torch's librccl, ncclCommInitRank,
+ncclAllReduce on the compute stream), and the executor's cross-rank code path
+(reduce -> all-reduce -> finalize / coefficients) with the EMU kind: W virtual ranks that
+hold identical data, whose sum is x·W. SyncBN over W identical replicas must give the
+single-process statistics (so identical outputs, dx and conv weight gradients) while
+dγ/dβ — computed from the globally summed Σdz, Σdz·ŷ like the Python SyncBN path —
+come out ×W.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _m():
+    from simclr_pytorch_distributed_amd.ops import _ext
+    return _ext.require()
+
+
+def test_rccl_single_rank_comm(gpu):
+    m = _m()
+    uid = m.rccl_unique_id()
+    assert uid.dtype == torch.uint8 and uid.numel() == 128
+    h = m.rccl_comm_init(uid, 1, 0)
+    try:
+        assert m.small_comm_world(h) == 1
+        for dt in (torch.float64, torch.float32):
+            x = torch.randn(1000, dtype=dt, device=gpu)
+            y = x.clone()
+            m.small_all_reduce_(h, y)
+            torch.cuda.synchronize()
+            assert torch.equal(x, y)
+    finally:
+        m.small_comm_destroy(h)
+
+
+def test_emu_comm_sum(gpu):
+    m = _m()
+    h = m.emu_small_comm(4)
+    x = torch.randn(64, dtype=torch.float64, device=gpu)
+    y = x.clone()
+    m.small_all_reduce_(h, y)
+    assert torch.equal(y, 4 * x)
+    m.small_comm_destroy(h)
+
+
+@pytest.mark.parametrize("which", ["layer1.0", "layer1.1", "layer2.0"])
+@pytest.mark.parametrize("name", ["resnet50", "resnet18"])
+def test_native_executor_syncbn_path(gpu, name, which):
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.ops import block
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    m = _m()
+    W = 2
+    h = m.emu_small_comm(W)
+    torch.manual_seed(0)
+    models = [SupConResNet(name).to(gpu).to(memory_format=torch.channels_last) for _ in range(2)]
+    models[1].load_state_dict(models[0].state_dict())
+    lay, idx = which.split(".")
+    cin = getattr(models[0].encoder, lay)[int(idx)].conv1.in_channels
+    x = torch.randn(8, 32, 32, cin, device=gpu).to(torch.bfloat16)
+    dout = None
+    res = []
+    for mdl, hh in zip(models, (0, h)):
+        flat = FlatParams(mdl)
+        runner = ModelRunner(mdl, "native", master=flat.flat, fused=True)
+        wc = runner.weight_cache()
+        wc.refresh()
+        blk = getattr(mdl.encoder, lay)[int(idx)]
+        info, params = block._block_info(blk)
+        flat.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        out = block._NativeBlock.apply(xi, blk, wc, True, info, hh, *params)
+        if dout is None:
+            dout = torch.randn_like(out)
+        out.backward(dout)
+        torch.cuda.synchronize()
+        res.append((out.detach().float(), xi.grad.float(), blk, flat))
+    (o0, dx0, b0, f0), (o1, dx1, b1, f1) = res
+    assert torch.equal(o0, o1)
+    assert torch.allclose(dx0, dx1, rtol=1e-2, atol=1e-3)
+    assert torch.equal(b0.bn1.running_mean, b1.bn1.running_mean)
+    assert torch.allclose(b0.conv1.weight.grad, b1.conv1.weight.grad, rtol=1e-3, atol=1e-5)
+    assert torch.allclose(b0.conv2.weight.grad, b1.conv2.weight.grad, rtol=1e-3, atol=1e-5)
+    for n in ("bn1", "bn2"):
+        g0, g1 = getattr(b0, n).weight.grad, getattr(b1, n).weight.grad
+        assert torch.allclose(W * g0, g1, rtol=1e-3, atol=1e-4), n
+        g0, g1 = getattr(b0, n).bias.grad, getattr(b1, n).bias.grad
+        assert torch.allclose(W * g0, g1, rtol=1e-3, atol=1e-4), n
+    m.small_comm_destroy(h)

@@ -23,11 +23,11 @@ def _free_port():
     return p
 
 
-def _launch(world, out):
+def _launch(world, out, syncbn_comm=""):
     port = _free_port()
     procs = []
     for r in range(world):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+        env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -41,12 +41,17 @@ def _launch(world, out):
         assert p.returncode == 0, err[-3000:]
 
 
-def test_two_rank_native_step_equals_single_rank(gpu, tmp_path):
+@pytest.mark.parametrize("syncbn_comm", ["", "xgmi"])
+def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, syncbn_comm):
+    """'': SyncBN statistics over gloo (Python block path); 'xgmi': the one-shot IPC arena
+    registered as a native handle, so the C++ block executor issues every BN all-reduce."""
     _launch(1, tmp_path)
-    _launch(2, tmp_path)
+    _launch(2, tmp_path, syncbn_comm)
     ref = torch.load(tmp_path / "w1_r0.pt", weights_only=True)
     a = torch.load(tmp_path / "w2_r0.pt", weights_only=True)
     b = torch.load(tmp_path / "w2_r1.pt", weights_only=True)
+    if syncbn_comm == "xgmi":
+        assert a["native_h"] > 0 and b["native_h"] > 0, "xGMI small communicator was not registered"
     bad = [n for n, o, k in zip(a["names"], a["offsets"], a["numels"])
            if not torch.equal(a["grad"][o:o + k], b["grad"][o:o + k])]
     assert not bad, f"all-reduced gradients differ across ranks for {len(bad)} params: {bad[:12]}"
