@@ -109,9 +109,10 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
   return {y, slab};
 }
 
-torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                         int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
-                         c10::optional<torch::Tensor> addend_mask) {
+// bs (optional): fused BN-backward statistics; its slab must hold conv_dgrad_slab_rows rows
+torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                              int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
+                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
   TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
@@ -147,9 +148,10 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
                 "addend_mask: uint8 [numel/8]");
     amask = addend_mask->data_ptr();
   }
+  if (bs) bs->row0 = 0;
   if (stride == 1) {
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                      cur_stream(), amask),
+                                      cur_stream(), amask, bs),
               "conv_dgrad");
     return dx;
   }
@@ -164,10 +166,67 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
       else
         wc = wt;   // no taps: the kernel writes zeros and never reads B
       check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                        cur_stream(), amask),
+                                        cur_stream(), amask, bs),
                 "conv_dgrad(class)");
+      if (bs) bs->row0 += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
     }
   return dx;
+}
+
+torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                         int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
+                         c10::optional<torch::Tensor> addend_mask) {
+  return conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, nullptr);
+}
+
+// dgrad + fused BN-backward statistics of dx for the BN whose pre-BN tensor is ya (and yb,
+// a second BN fed by the same gradient: projection shortcut). ReLU mask from `mask_bits`
+// (1 bit per element) or recomputed as ya·msc + msh > 0. Returns [dx, slab [rows][2|3][C]].
+std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W,
+                                             int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
+                                             OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
+                                             OptT mask_bits, OptT msc, OptT msh) {
+  check_bf16_nhwc(ya, "ya");
+  const int64_t C = wt.size(0);
+  TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
+  check_vec(ma, C, "ma");
+  BnBwdStat bs{};
+  bs.ya = ya.data_ptr();
+  bs.ma = ma.data_ptr<float>();
+  if (yb.has_value()) {
+    check_bf16_nhwc(*yb, "yb");
+    TORCH_CHECK(yb->sizes() == ya.sizes(), "yb shape");
+    TORCH_CHECK(mb.has_value(), "mb required with yb");
+    check_vec(*mb, C, "mb");
+    bs.yb = yb->data_ptr();
+    bs.mb = mb->data_ptr<float>();
+  }
+  if (mask_bits.has_value()) {
+    TORCH_CHECK(mask_bits->is_cuda() && mask_bits->scalar_type() == at::kByte && mask_bits->is_contiguous() &&
+                    mask_bits->numel() * 8 == ya.numel(),
+                "mask_bits: uint8 [numel/8]");
+    bs.mask = mask_bits->data_ptr<uint8_t>();
+  } else if (msc.has_value()) {
+    TORCH_CHECK(msh.has_value(), "msh required with msc");
+    check_vec(*msc, C, "msc");
+    check_vec(*msh, C, "msh");
+    bs.msc = msc->data_ptr<float>();
+    bs.msh = msh->data_ptr<float>();
+  }
+  ConvGeom g{};
+  g.N = dy.size(0); g.P = dy.size(1); g.Q = dy.size(2); g.K = dy.size(3);
+  g.C = C; g.R = wt.size(1); g.S = wt.size(2);
+  g.H = H; g.W = W; g.stride = stride; g.pad = pad;
+  const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
+  if (cfg < 0) cfg = auto_cfg(M, g.C, (int64_t)g.R * g.S * g.K / (stride * stride), true);
+  int rows = 0;
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) rows += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
+  const int ns = yb.has_value() ? 3 : 2;
+  auto slab = torch::empty({rows, ns, C}, dy.options().dtype(at::kFloat));
+  bs.slab = slab.data_ptr<float>();
+  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs);
+  return {dx, slab};
 }
 
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
@@ -645,6 +704,44 @@ hipEvent_t next_event() {
   return e;
 }
 
+// BN-backward coefficients from a fused-dgrad statistics slab [rows][2|3][C]: one column
+// reduction whose last block evaluates the coefficients, or (communicator of >1 ranks)
+// reduce -> in-place all-reduce -> coefficients
+std::vector<torch::Tensor> bn_bwd_coef_slab(int64_t comm, torch::Tensor slab, double count, OptT g_a,
+                                            torch::Tensor mean_a, torch::Tensor inv_a, OptT g_b, OptT mean_b,
+                                            OptT inv_b, OptT sink_ga, OptT sink_ba, OptT sink_gb, OptT sink_bb) {
+  TORCH_CHECK(slab.dim() == 3 && (slab.size(1) == 2 || slab.size(1) == 3), "slab: [rows][2|3][C]");
+  check_slab(slab, slab.size(1));
+  c10::DeviceGuard dg(slab.device());
+  const int64_t rows = slab.size(0), nsum = slab.size(1), C = slab.size(2);
+  auto sums = torch::empty({nsum, C}, slab.options().dtype(at::kDouble));
+  auto scratch = reduce_scratch(slab, rows, nsum, C);
+  if (comm != 0 && small_comm_world(comm) > 1) {
+    check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, (int)nsum, C, scratch.data_ptr<double>(),
+                                reduce_counters(slab.device()), sums.data_ptr<double>(), 0, nullptr, nullptr,
+                                cur_stream()),
+              "bn_bwd_coef_slab(reduce)");
+    small_all_reduce_(comm, sums);
+    return bn_bwd_coef(sums, count * small_comm_world(comm), g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga, sink_ba,
+                       sink_gb, sink_bb);
+  }
+  CoefOut o;
+  const BnCoefArgs a = coef_args(slab, C, (int)nsum - 1, count, g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga,
+                                 sink_ba, sink_gb, sink_bb, o);
+  check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, (int)nsum, C, scratch.data_ptr<double>(),
+                              reduce_counters(slab.device()), sums.data_ptr<double>(), 2, nullptr, &a, cur_stream()),
+            "bn_bwd_coef_slab");
+  return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
+}
+
+bool dgrad_bnstat_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SDX_DGRAD_BNSTAT");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 // dW (+)= wgrad(dy, x) into the parameter's gradient sink, on the side stream if given
 void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                 const torch::Tensor& sink, int64_t side) {
@@ -730,9 +827,17 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
 // bnst: [sc, sh, mu, iv] per BN (fwd order)
 // wt: dgrad-layout weights (conv order); dw: fp32 gradient sinks (conv order);
 // bng: [gamma, dgamma_sink, dbeta_sink] per BN. Returns dx.
-torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, std::vector<torch::Tensor> bnst,
-                        std::vector<torch::Tensor> wt, std::vector<torch::Tensor> dw, std::vector<torch::Tensor> bng,
-                        int64_t stride, bool bottleneck, bool proj, int64_t side, int64_t comm) {
+//
+// Cross-block BN-statistics hand-off (SDX_DGRAD_BNSTAT): in_slab (optional) holds this
+// block's OUTPUT-BN backward sums [rows][2|3][C], computed by the NEXT block's final dgrad
+// (the one that produced dout); prev = [y_last, mean_last, y_short|-, mean_short|-, omask]
+// of the PREVIOUS native block (whose output is x): the final dgrad here computes that
+// block's sums from the dx it stores. Returns [dx, slab for the previous block | undefined].
+std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved,
+                                     std::vector<torch::Tensor> bnst, std::vector<torch::Tensor> wt,
+                                     std::vector<torch::Tensor> dw, std::vector<torch::Tensor> bng, int64_t stride,
+                                     bool bottleneck, bool proj, int64_t side, int64_t comm, OptT in_slab,
+                                     std::vector<torch::Tensor> prev) {
   const int nconv = bottleneck ? 3 : 2;
   const int nbn = nconv + (proj ? 1 : 0);
   TORCH_CHECK((int)wt.size() == nbn && (int)dw.size() == nbn && (int)bng.size() == 3 * nbn &&
@@ -747,17 +852,25 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
   const torch::Tensor& ylast = bottleneck ? y3 : y2;
   const double cnt_last = rows_of(ylast), cnt1 = rows_of(y1);
   torch::Tensor dylast, dys, dz;
+  const bool have_slab = in_slab.has_value() && in_slab->defined() && in_slab->numel() > 0;
+  if (have_slab) TORCH_CHECK(in_slab->size(1) == (proj ? 3 : 2), "block_bwd: in_slab set count");
   if (proj) {
-    auto c = bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), ys, S(nconv, 2), c10::nullopt, c10::nullopt,
-                                cnt_last, G(lastbn, 0), S(lastbn, 3), G(nconv, 0), S(nconv, 3), G(lastbn, 1),
-                                G(lastbn, 2), G(nconv, 1), G(nconv, 2));
+    auto c = have_slab
+                 ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), G(nconv, 0),
+                                    S(nconv, 2), S(nconv, 3), G(lastbn, 1), G(lastbn, 2), G(nconv, 1), G(nconv, 2))
+                 : bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), ys, S(nconv, 2), c10::nullopt, c10::nullopt,
+                               cnt_last, G(lastbn, 0), S(lastbn, 3), G(nconv, 0), S(nconv, 3), G(lastbn, 1),
+                               G(lastbn, 2), G(nconv, 1), G(nconv, 2));
     auto r = bn_bwd_apply(dout, out, ylast, c[0], ys, c[1], false, c10::nullopt, c10::nullopt);
     dylast = r[0];
     dys = r[1];
   } else {
-    auto c = bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
-                                c10::nullopt, cnt_last, G(lastbn, 0), S(lastbn, 3), c10::nullopt, c10::nullopt,
-                                G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt);
+    auto c = have_slab
+                 ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), c10::nullopt,
+                                    c10::nullopt, c10::nullopt, G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt)
+                 : bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
+                               c10::nullopt, cnt_last, G(lastbn, 0), S(lastbn, 3), c10::nullopt, c10::nullopt,
+                               G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt);
     // identity shortcut: its gradient dz = dout·[out > 0] is never materialised when the ReLU
     // bitmask is available — the last dgrad epilogue adds dout under the mask
     const bool bitmask = out.scalar_type() == at::kByte;
@@ -765,42 +878,64 @@ torch::Tensor block_bwd(torch::Tensor dout, std::vector<torch::Tensor> saved, st
     dylast = r[0];
     dz = bitmask ? torch::Tensor() : r[2];
   }
+  // dgrad whose output da is the gradient of the block-internal BN i's ReLU output; the BN's
+  // Σda·m, Σda·m·(y−μ) come from the dgrad epilogue (SDX_DGRAD_BNSTAT=0: separate pass)
+  auto dgrad_bn = [&](const torch::Tensor& dyo, const torch::Tensor& w, const torch::Tensor& y, int64_t st,
+                      int64_t pad, int i, double cnt) -> std::pair<torch::Tensor, torch::Tensor> {
+    if (dgrad_bnstat_enabled()) {
+      auto r = conv_dgrad_bnstat(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt,
+                                 c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0), S(i, 1));
+      auto c = bn_bwd_coef_slab(comm, r[1], cnt, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt,
+                                c10::nullopt, G(i, 1), G(i, 2), c10::nullopt, c10::nullopt);
+      return {r[0], c[0]};
+    }
+    auto da = conv_dgrad(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt, c10::nullopt);
+    auto c = bn_bwd_sync(comm, da, c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, S(i, 0), S(i, 1), cnt,
+                         G(i, 0), S(i, 3), c10::nullopt, c10::nullopt, G(i, 1), G(i, 2), c10::nullopt, c10::nullopt);
+    return {da, c[0]};
+  };
   torch::Tensor dy1;
   if (bottleneck) {
     side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
-    auto da2 = conv_dgrad(dylast, wt[2], y2.size(1), y2.size(2), 1, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    auto c2 = bn_bwd_sync(comm, da2, c10::nullopt, y2, S(1, 2), c10::nullopt, c10::nullopt, S(1, 0), S(1, 1),
-                                 cnt_last, G(1, 0), S(1, 3), c10::nullopt, c10::nullopt, G(1, 1), G(1, 2),
-                                 c10::nullopt, c10::nullopt);
-    auto dy2 = bn_bwd_apply(da2, c10::nullopt, y2, c2[0], c10::nullopt, c10::nullopt, false, S(1, 0), S(1, 1))[0];
+    auto r2 = dgrad_bn(dylast, wt[2], y2, 1, 0, 1, cnt_last);
+    auto dy2 = bn_bwd_apply(r2.first, c10::nullopt, y2, r2.second, c10::nullopt, c10::nullopt, false, S(1, 0),
+                            S(1, 1))[0];
     side_wgrad(dy2, a1, 3, 3, stride, 1, dw[1], side);
-    auto da1 = conv_dgrad(dy2, wt[1], H, W, stride, 1, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    auto c1 = bn_bwd_sync(comm, da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
-                                 cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
-                                 c10::nullopt);
-    dy1 = bn_bwd_apply(da1, c10::nullopt, y1, c1[0], c10::nullopt, c10::nullopt, false, S(0, 0), S(0, 1))[0];
+    auto r1 = dgrad_bn(dy2, wt[1], y1, stride, 1, 0, cnt1);
+    dy1 = bn_bwd_apply(r1.first, c10::nullopt, y1, r1.second, c10::nullopt, c10::nullopt, false, S(0, 0),
+                       S(0, 1))[0];
     side_wgrad(dy1, x, 1, 1, 1, 0, dw[0], side);
   } else {
     side_wgrad(dylast, a1, 3, 3, 1, 1, dw[1], side);
-    auto da1 = conv_dgrad(dylast, wt[1], y1.size(1), y1.size(2), 1, 1, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    auto c1 = bn_bwd_sync(comm, da1, c10::nullopt, y1, S(0, 2), c10::nullopt, c10::nullopt, S(0, 0), S(0, 1),
-                                 cnt1, G(0, 0), S(0, 3), c10::nullopt, c10::nullopt, G(0, 1), G(0, 2), c10::nullopt,
-                                 c10::nullopt);
-    dy1 = bn_bwd_apply(da1, c10::nullopt, y1, c1[0], c10::nullopt, c10::nullopt, false, S(0, 0), S(0, 1))[0];
+    auto r1 = dgrad_bn(dylast, wt[1], y1, 1, 1, 0, cnt1);
+    dy1 = bn_bwd_apply(r1.first, c10::nullopt, y1, r1.second, c10::nullopt, c10::nullopt, false, S(0, 0),
+                       S(0, 1))[0];
     side_wgrad(dy1, x, 3, 3, stride, 1, dw[0], side);
   }
   const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
+  // the final dgrad (the one that stores dx) optionally emits the previous block's output-BN sums
+  const bool want_prev = dgrad_bnstat_enabled() && prev.size() == 5 && prev[4].defined() && prev[4].numel() > 0;
+  torch::Tensor prev_slab;
+  auto last_dgrad = [&](OptT o, OptT add, OptT amask) -> torch::Tensor {
+    if (!want_prev) return conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, o, add, amask);
+    const bool two = prev[2].defined() && prev[2].numel() > 0;
+    auto r = conv_dgrad_bnstat(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, prev[0], prev[1],
+                               two ? OptT(prev[2]) : OptT(), two ? OptT(prev[3]) : OptT(), prev[4], c10::nullopt,
+                               c10::nullopt);
+    prev_slab = r[1];
+    return r[0];
+  };
   torch::Tensor dx;
   if (proj) {
     side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);
     dx = conv_dgrad(dys, wt[nconv], H, W, stride, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, dx, dx, c10::nullopt);
+    dx = last_dgrad(dx, dx, c10::nullopt);
   } else if (dz.defined()) {
-    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, c10::nullopt, dz, c10::nullopt);
+    dx = last_dgrad(c10::nullopt, dz, c10::nullopt);
   } else {
-    dx = conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, c10::nullopt, dout, out);
+    dx = last_dgrad(c10::nullopt, dout, out);
   }
-  return dx;
+  return {dx, prev_slab};
 }
 
 }  // namespace
@@ -843,6 +978,20 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("inv_b") = pybind11::none(), pybind11::arg("sink_ga") = pybind11::none(),
         pybind11::arg("sink_ba") = pybind11::none(), pybind11::arg("sink_gb") = pybind11::none(),
         pybind11::arg("sink_bb") = pybind11::none());
+  m.def("conv_dgrad_bnstat", &conv_dgrad_bnstat,
+        "dgrad + fused BN-backward statistics of dx (slab [rows][2|3][C] for bn_bwd_coef_slab)",
+        pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("stride"),
+        pybind11::arg("pad"), pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none(),
+        pybind11::arg("ya"), pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(),
+        pybind11::arg("mb") = pybind11::none(), pybind11::arg("mask_bits") = pybind11::none(),
+        pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none());
+  m.def("bn_bwd_coef_slab", &bn_bwd_coef_slab, "BN-backward coefficients (+dγ/dβ into sinks) from a dgrad stat slab",
+        pybind11::arg("comm"), pybind11::arg("slab"), pybind11::arg("count"), pybind11::arg("g_a"),
+        pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),
+        pybind11::arg("mean_b") = pybind11::none(), pybind11::arg("inv_b") = pybind11::none(),
+        pybind11::arg("sink_ga") = pybind11::none(), pybind11::arg("sink_ba") = pybind11::none(),
+        pybind11::arg("sink_gb") = pybind11::none(), pybind11::arg("sink_bb") = pybind11::none());
   m.def("block_fwd", &block_fwd, "native residual-block forward (whole kernel sequence; comm: SyncBN handle or 0)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bn"), pybind11::arg("stride"),
         pybind11::arg("bottleneck"), pybind11::arg("proj"), pybind11::arg("training"), pybind11::arg("eps"),
@@ -850,7 +999,8 @@ void register_conv_bn(pybind11::module& m) {
   m.def("block_bwd", &block_bwd, "native residual-block backward (dgrad chain + side-stream wgrads)",
         pybind11::arg("dout"), pybind11::arg("saved"), pybind11::arg("bnst"), pybind11::arg("wt"),
         pybind11::arg("dw"), pybind11::arg("bng"), pybind11::arg("stride"), pybind11::arg("bottleneck"),
-        pybind11::arg("proj"), pybind11::arg("side"), pybind11::arg("comm") = 0);
+        pybind11::arg("proj"), pybind11::arg("side"), pybind11::arg("comm") = 0,
+        pybind11::arg("in_slab") = pybind11::none(), pybind11::arg("prev") = std::vector<torch::Tensor>());
   m.def("bn_bwd_apply", &bn_bwd_apply, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
         pybind11::arg("ca"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("cb") = pybind11::none(),
         pybind11::arg("want_dz") = false, pybind11::arg("msc") = pybind11::none(),

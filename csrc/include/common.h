@@ -56,6 +56,30 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, r);
 }
 
+// compile-time loop: f(std::integral_constant<int, i>) for i in [B, E) — for bodies that
+// index register arrays, which a runtime (not fully unrolled) loop would place in scratch
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// 8 packed bf16 (16 B) <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+}
+
 // Sum over the 16 lanes of each DPP row (lanes 16r..16r+15), result in every lane of the
 // row: 4 DPP-modified adds (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror),
 // no LDS traffic (a __shfl_xor lowers to ds_bpermute).

@@ -28,6 +28,21 @@ struct ConvGeom {
   int P, Q;         // output spatial
   int stride, pad;
 };
+// DGRAD epilogue BatchNorm-backward statistics of the stored dx (= the output gradient of
+// the BN whose input the conv read): per M-tile Σd·m, Σd·m·(ya−μa) [, Σd·m·(yb−μb)] with
+// m the ReLU mask — bitmask bit (mask), or ya·msc + msh > 0 (msc/msh), or 1 — written to
+// slab row row0 + m_tile of a [rows][2|3][C] fp32 slab (reduced like the forward stats).
+struct BnBwdStat {
+  float* slab;
+  const void* ya;
+  const float* ma;
+  const void* yb;        // optional second BN (projection shortcut) reading the same dx
+  const float* mb;
+  const uint8_t* mask;   // 1 bit per dx element
+  const float* msc;
+  const float* msh;
+  int row0;
+};
 int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
@@ -37,7 +52,10 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
-                                   const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr);
+                                   const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
+                                   const BnBwdStat* bstat = nullptr);
+// M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
+int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
 // partial: fp32 [splits][K][R*S*C] workspace (unused when splits == 1 and !accumulate)
 hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,

@@ -20,19 +20,6 @@ using namespace sdx;
 
 namespace {
 
-__device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
-__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
-  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
-}
-
 // ---- per-channel epilogues (shared by the stand-alone kernels and the fused reduction) ----
 // (Σy, Σy²) over `count` rows -> scale/shift, mean/invstd (for backward), running stats
 // (unbiased variance, as torch BatchNorm2d)

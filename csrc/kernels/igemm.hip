@@ -63,6 +63,8 @@ struct IgemmParams {
   const uint8_t* addend_mask;
   // operand sizes in elements (bounds checks of the checked build)
   long a_elems, b_elems;
+  // DGRAD: fused BN-backward statistics of the stored output (BnBwdStat; bs.slab null = off)
+  BnBwdStat bs;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -136,7 +138,9 @@ struct Tile {
 // (global_load_lds) staging of both K-inner operands (FWD / DGRAD without the BN prologue):
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
-template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
+// BST (DGRAD only): fused BN-backward statistics epilogue (p.bs) — a separate variant so
+// the plain dgrad keeps its register budget.
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, bool BST>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
   using T = Tile<MODE, BM, BN, NT>;
@@ -702,6 +706,59 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     for (int j = 0; j < TN; ++j)
       ov[i][j] = make_uint2(pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3]));
 
+  // Store loop: thread tid writes the 16-B chunks e = tid + it·NT (it < ITER) of the
+  // [BM][BN] tile — always the same column chunk my_ch. The epilogue's own global operands
+  // (DGRAD: residual addend + its ReLU bits; fused BN-backward statistics: y_a, y_b + ReLU
+  // bits) are prefetched PF iterations ahead through a register ring, the first PF issued
+  // before the LDS staging, so their latency overlaps it instead of stalling every chunk.
+  constexpr int CPR = BN / 8;
+  constexpr int ITER = BM * CPR / NT;
+  constexpr int PF = ITER < 4 ? ITER : 4;
+  static_assert(NT % CPR == 0 && CPR <= 64 && (BM * CPR) % NT == 0, "fixed column chunk per thread");
+  const bool has_add = MODE == MODE_DGRAD && p.addend != nullptr;
+  constexpr bool bst = MODE == MODE_DGRAD && BST;
+  const int my_ch = tid % CPR, my_col = n0 + my_ch * 8;
+  int eo[ITER];   // output element offset of each chunk (-1: outside the tensor)
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int row = (tid + it * NT) / CPR;
+    const int m = m0 + row;
+    int o = -1;
+    if (m < p.M && my_col < p.Ncol) {
+      int orow = m;
+      if (MODE == MODE_DGRAD && g.stride != 1) {
+        const int hw = p.Hc * p.Wc;
+        const int n = m / hw, rem = m - n * hw;
+        const int yy = rem / p.Wc, xx = rem - yy * p.Wc;
+        orow = (n * g.H + yy * g.stride + p.ph) * g.W + xx * g.stride + p.pw;
+      }
+      o = orow * p.Ncol + my_col;
+    }
+    eo[it] = o;
+  }
+  uint4 pf_add[PF], pf_ya[PF], pf_yb[PF];
+  uint32_t pf_am[PF], pf_bm[PF];
+  auto prefetch = [&](auto IT, auto SL) __attribute__((always_inline)) {
+    constexpr int it = decltype(IT)::value, sl = decltype(SL)::value;
+    const int o = eo[it];
+    const bool ok = o >= 0;
+    if (MODE == MODE_DGRAD && has_add) {
+      // (the zero page, not a private zero: a select between a global and a private
+      // address would turn the load into a flat load and spill the zero to scratch)
+      pf_add[sl] = ld16_or_zero(p.addend + (ok ? o : 0), ok);
+      pf_am[sl] = (ok && p.addend_mask != nullptr) ? (uint32_t)p.addend_mask[o >> 3] : 0xffu;
+    }
+    if (MODE == MODE_DGRAD && bst) {
+      pf_ya[sl] = ld16_or_zero(reinterpret_cast<const uint16_t*>(p.bs.ya) + (ok ? o : 0), ok);
+      const bool okb = ok && p.bs.yb != nullptr;
+      pf_yb[sl] = ld16_or_zero(reinterpret_cast<const uint16_t*>(p.bs.yb) + (okb ? o : 0), okb);
+      pf_bm[sl] = (ok && p.bs.mask != nullptr) ? (uint32_t)p.bs.mask[o >> 3] : 0xffu;
+    }
+  };
+  if (MODE == MODE_DGRAD && (has_add || bst)) {
+    static_for<0, PF>([&](auto I) { prefetch(I, I); });
+  }
+
   // stage the C tile through LDS ([BM][BN] bf16, rows padded by 8 B: 16 lanes writing 8 B
   // at the same column of 16 consecutive rows hit distinct banks)
   constexpr int CRS = BN * 2 + 8;
@@ -712,36 +769,49 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     for (int j = 0; j < TN; ++j)
       *reinterpret_cast<uint2*>(smem + (wm * WTM + 16 * i + c) * CRS + (wn * WTN + 16 * j + 4 * h) * 2) = ov[i][j];
   __syncthreads();
+  // fused BN-backward statistics (DGRAD): per-thread sums for column chunk my_ch
+  const int bs_ns = p.bs.yb != nullptr ? 3 : 2;
+  float bmu_a[8], bmu_b[8], bmk_s[8], bmk_t[8], bsum[3][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bmu_a[q] = bmu_b[q] = bmk_s[q] = bmk_t[q] = 0.f;
+    bsum[0][q] = bsum[1][q] = bsum[2][q] = 0.f;
+  }
+  if (MODE == MODE_DGRAD && bst && my_col < p.Ncol) {
+    load8f(p.bs.ma + my_col, bmu_a);
+    if (p.bs.yb) load8f(p.bs.mb + my_col, bmu_b);
+    if (p.bs.mask == nullptr && p.bs.msc != nullptr) {
+      load8f(p.bs.msc + my_col, bmk_s);
+      load8f(p.bs.msh + my_col, bmk_t);
+    }
+  }
   {
     uint16_t* out = reinterpret_cast<uint16_t*>(p.out);
-    constexpr int CPR = BN / 8;
-    for (int e = tid; e < BM * CPR; e += NT) {
-      const int row = e / CPR, ch = e % CPR;
-      const int m = m0 + row, col = n0 + ch * 8;
-      if (m < p.M && col < p.Ncol) {
-        const unsigned char* src = smem + row * CRS + ch * 16;
+    static_for<0, ITER>([&](auto I) {
+      constexpr int it = decltype(I)::value, sl = it % PF;
+      const uint4 a_in = pf_add[sl], ya_in = pf_ya[sl], yb_in = pf_yb[sl];
+      const uint32_t am = pf_am[sl], bm = pf_bm[sl];
+      if constexpr (it + PF < ITER) {
+        if (MODE == MODE_DGRAD && (has_add || bst))
+          prefetch(std::integral_constant<int, it + PF>{}, std::integral_constant<int, sl>{});
+      }
+      const int o = eo[it];
+      if (o >= 0) {
+        const int row = (tid + it * NT) / CPR;
+        const unsigned char* src = smem + row * CRS + my_ch * 16;
         const uint2 lo = *reinterpret_cast<const uint2*>(src);
         const uint2 hi = *reinterpret_cast<const uint2*>(src + 8);
-        int orow = m;
-        if (MODE == MODE_DGRAD && g.stride != 1) {
-          const int hw = p.Hc * p.Wc;
-          const int n = m / hw, rem = m - n * hw;
-          const int yy = rem / p.Wc, xx = rem - yy * p.Wc;
-          orow = (n * g.H + yy * g.stride + p.ph) * g.W + xx * g.stride + p.pw;
-        }
         uint4 v = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        if (MODE == MODE_DGRAD && p.addend != nullptr) {
-          // fused residual-gradient accumulation: out = dgrad + addend (may alias out)
-          uint4 a = *reinterpret_cast<const uint4*>(p.addend + (size_t)orow * p.Ncol + col);
-          if (p.addend_mask != nullptr) {
-            // addend = dout·[out > 0] from the block output's 1-bit ReLU mask (no dz tensor)
-            const uint32_t mb = p.addend_mask[((size_t)orow * p.Ncol + col) >> 3];
-            uint32_t* aw2 = reinterpret_cast<uint32_t*>(&a);
+        if (MODE == MODE_DGRAD && has_add) {
+          // fused residual-gradient accumulation: out = dgrad + addend (may alias out: every
+          // chunk is read and written by the same thread); with addend_mask the addend is
+          // dout·[out > 0] from the block output's 1-bit ReLU mask (no dz tensor)
+          uint4 a = a_in;
+          uint32_t* aw2 = reinterpret_cast<uint32_t*>(&a);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const uint32_t keep = ((mb >> (2 * q)) & 1u ? 0x0000ffffu : 0u) | ((mb >> (2 * q + 1)) & 1u ? 0xffff0000u : 0u);
-              aw2[q] &= keep;
-            }
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t keep = ((am >> (2 * q)) & 1u ? 0x0000ffffu : 0u) | ((am >> (2 * q + 1)) & 1u ? 0xffff0000u : 0u);
+            aw2[q] &= keep;
           }
           const uint32_t* vw = reinterpret_cast<const uint32_t*>(&v);
           const uint32_t* aw = reinterpret_cast<const uint32_t*>(&a);
@@ -754,8 +824,59 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
           }
           v = make_uint4(r[0], r[1], r[2], r[3]);
         }
-        *reinterpret_cast<uint4*>(out + (size_t)orow * p.Ncol + col) = v;
+        *reinterpret_cast<uint4*>(out + o) = v;
+        if (MODE == MODE_DGRAD && bst) {
+          // statistics of the stored (bf16-rounded) values, as bn_bwd_reduce would read them
+          float d[8], ya[8];
+          unpack8(v, d);
+          unpack8(ya_in, ya);
+          if (p.bs.mask != nullptr) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) d[q] = (bm >> q) & 1u ? d[q] : 0.f;
+          } else if (p.bs.msc != nullptr) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) d[q] = ya[q] * bmk_s[q] + bmk_t[q] > 0.f ? d[q] : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            bsum[0][q] += d[q];
+            bsum[1][q] = fmaf(d[q], ya[q] - bmu_a[q], bsum[1][q]);
+          }
+          if (p.bs.yb != nullptr) {
+            float yb[8];
+            unpack8(yb_in, yb);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bsum[2][q] = fmaf(d[q], yb[q] - bmu_b[q], bsum[2][q]);
+          }
+        }
       }
+    });
+  }
+
+  if (MODE == MODE_DGRAD && bst) {
+    // lanes my_ch, my_ch + CPR, ... of a wave hold the same columns: butterfly over them,
+    // then one [NS][BN] row per wave through LDS, summed in wave order (deterministic)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        for (int off = CPR; off < 64; off <<= 1) bsum[k][q] += __shfl_xor(bsum[k][q], off);
+    __syncthreads();   // C-tile reads of the store loop are done
+    float* red = reinterpret_cast<float*>(smem);   // [NT/64][3][BN]
+    static_assert((NT / 64) * 3 * BN * 4 <= LDS, "BN-bwd stat reduction must fit the staging LDS");
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) red[(wv * 3 + k) * BN + my_ch * 8 + q] = bsum[k][q];
+    }
+    __syncthreads();
+    for (int e = tid; e < bs_ns * BN; e += NT) {
+      const int k = e / BN, col = e % BN;
+      float s = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NT / 64; ++w2) s += red[(w2 * 3 + k) * BN + col];
+      if (n0 + col < p.Ncol) p.bs.slab[((size_t)(p.bs.row0 + mt) * bs_ns + k) * p.Ncol + n0 + col] = s;
     }
   }
 
@@ -865,6 +986,20 @@ int igemm_ablate() {
   return a;
 }
 
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
+hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
+  if constexpr (MODE == MODE_DGRAD) {
+    if (bs) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+  }
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 template <int MODE, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   p.ablate = igemm_ablate();
@@ -874,25 +1009,22 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   // depth 2 only where the second register stage fits without spilling (checked with
   // -Rpass-analysis=kernel-resource-usage)
   constexpr bool kDepth2 = (BM == 64 && BN == 64) || (MODE == MODE_FWD && BM != 256);
+  const bool bs = MODE == MODE_DGRAD && p.bs.slab != nullptr;
   {
     // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
     // (SDX_IGEMM_GLDS=2 enables it there too)
     if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 3>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
-      SDX_LAUNCH_CHECK();
-      return hipSuccess;
+      return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
     }
   }
   if constexpr (kDepth2) {
-    if (igemm_depth() == 2) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+    if (igemm_depth() == 2 && !bs) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
   }
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 1>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
-  SDX_LAUNCH_CHECK();
-  return hipSuccess;
+  return launch_k<MODE, BM, BN, WM, WN, 1>(bs, grid, p, s);
 }
 
 // tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
@@ -950,9 +1082,18 @@ void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* 
   *Wc = pw < g.W ? (g.W - pw + st - 1) / st : 0;
 }
 
+int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
+  int r0, nr, s0, ns, Hc, Wc;
+  conv_dgrad_class(g, ph, pw, &r0, &nr, &s0, &ns, &Hc, &Wc);
+  const int M = g.N * Hc * Wc, bm = igemm_tile_m(cfg);
+  return (M + bm - 1) / bm;
+}
+
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
-                                   const void* addend, int cfg, hipStream_t s, const void* addend_mask) {
+                                   const void* addend, int cfg, hipStream_t s, const void* addend_mask,
+                                   const BnBwdStat* bstat) {
   IgemmParams p{};
+  if (bstat != nullptr) p.bs = *bstat;
   p.addend_mask = (const uint8_t*)addend_mask;
   p.g = g;
   p.a = (const uint16_t*)dy;

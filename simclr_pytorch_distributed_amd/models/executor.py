@@ -122,9 +122,10 @@ class ModelRunner:
         wc.refresh()
         g = self.sync_group
         out = fb.stem(x, enc, wc, training, g)
+        chain = fb.BlockChain()
         for blk in enc.blocks():
-            out = fb.bottleneck(out, blk, wc, training, g) if isinstance(blk, Bottleneck) else \
-                fb.basic(out, blk, wc, training, g)
+            out = fb.bottleneck(out, blk, wc, training, g, chain) if isinstance(blk, Bottleneck) else \
+                fb.basic(out, blk, wc, training, g, chain)
         if training and self._nbt:
             torch._foreach_add_(self._nbt, 1)
         return global_avgpool_nhwc(out)

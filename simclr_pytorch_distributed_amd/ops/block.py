@@ -284,6 +284,28 @@ class _Stem(torch.autograd.Function):
         return (None, None, None, None, None) + (None,) * len(ctx.params)
 
 
+class BlockLink:
+    """Hand-off between two consecutive native blocks i -> i+1 (one per forward pass).
+
+    ``prev``: block i's ``[y_last, mean_last, y_shortcut|-, mean_shortcut|-, out bitmask]``,
+    read by block i+1's backward, whose final dgrad (the kernel that stores dL/d out_i)
+    emits block i's output-BN backward sums in its epilogue; ``slab`` carries them back to
+    block i's backward, which then skips its separate reduction pass over dout."""
+    __slots__ = ("prev", "slab")
+
+    def __init__(self):
+        self.prev = None
+        self.slab = None
+
+
+class BlockChain:
+    """Threads :class:`BlockLink` objects through one encoder forward."""
+    __slots__ = ("last",)
+
+    def __init__(self):
+        self.last = None
+
+
 class _NativeBlock(torch.autograd.Function):
     """Whole residual block through the native executor (csrc/bindings/conv_bn_ops.cpp
     ``block_fwd`` / ``block_bwd``): one host call per block and direction instead of
@@ -294,7 +316,7 @@ class _NativeBlock(torch.autograd.Function):
     itself, in place on the compute stream (0 = single-process statistics)."""
 
     @staticmethod
-    def forward(ctx, x, blk, wc, training, info, comm_h, *params):
+    def forward(ctx, x, blk, wc, training, info, comm_h, link_in, link_out, *params):
         m = _ext.require()
         convs, bns, bottle, proj = info
         bn0 = bns[0]
@@ -310,6 +332,12 @@ class _NativeBlock(torch.autograd.Function):
             saved = [x] + [t if t is not None else e for t in r[1:7]] + [r[7]]
             ctx.save_for_backward(*saved, *r[8:])
             ctx.blk, ctx.wc, ctx.info, ctx.params, ctx.comm_h = blk, wc, info, params, comm_h
+            ctx.link_in, ctx.link_out = link_in, link_out
+            if link_out is not None:
+                nconv = 3 if bottle else 2
+                st = r[8:]
+                link_out.prev = [r[5] if bottle else r[3], st[4 * (nconv - 1) + 2],
+                                 r[6] if proj else e, st[4 * nconv + 2] if proj else _empty_f(x), r[7]]
         return out
 
     @staticmethod
@@ -323,13 +351,25 @@ class _NativeBlock(torch.autograd.Function):
             bng += [bn.weight.detach(), sinks.target(bn.weight), sinks.target(bn.bias)]
         from . import streams
         side = streams.side(dout.device).cuda_stream if streams.ENABLED else 0
-        dx = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
-                         [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side, ctx.comm_h)
+        lin, lout = ctx.link_in, ctx.link_out
+        in_slab = lout.slab if lout is not None else None
+        prev = lin.prev if (lin is not None and lin.prev is not None) else []
+        dx, pslab = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
+                                [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side,
+                                ctx.comm_h, in_slab, prev)
+        if lout is not None:
+            lout.slab = lout.prev = None
+        if lin is not None:
+            lin.slab = pslab if (pslab is not None and pslab.numel() > 0) else None
         sinks.notify(ctx.params)
-        return (dx, None, None, None, None, None) + (None,) * len(ctx.params)
+        return (dx, None, None, None, None, None, None, None) + (None,) * len(ctx.params)
 
 
 _EMPTY = {}
+
+
+def _empty_f(like):
+    return _empty(torch.empty(0, dtype=torch.float32, device=like.device))
 
 
 def _empty(like):
@@ -372,19 +412,31 @@ def block_params(mod) -> List[torch.nn.Parameter]:
     return list(info[1]) if info is not None else [p for p in mod.parameters()]
 
 
-def bottleneck(x, blk, wc, training: bool, group=None):
+def bottleneck(x, blk, wc, training: bool, group=None, chain: Optional[BlockChain] = None):
     info, params = _block_info(blk)
     h = _native_comm(group, info)
     if h >= 0:
-        return _NativeBlock.apply(x, blk, wc, training, info, h, *params)
+        lin = chain.last if chain is not None else None
+        lout = BlockLink() if (chain is not None and training) else None
+        if chain is not None:
+            chain.last = lout
+        return _NativeBlock.apply(x, blk, wc, training, info, h, lin, lout, *params)
+    if chain is not None:
+        chain.last = None
     return _Bottleneck.apply(x, blk, wc, training, group, *params)
 
 
-def basic(x, blk, wc, training: bool, group=None):
+def basic(x, blk, wc, training: bool, group=None, chain: Optional[BlockChain] = None):
     info, params = _block_info(blk)
     h = _native_comm(group, info)
     if h >= 0:
-        return _NativeBlock.apply(x, blk, wc, training, info, h, *params)
+        lin = chain.last if chain is not None else None
+        lout = BlockLink() if (chain is not None and training) else None
+        if chain is not None:
+            chain.last = lout
+        return _NativeBlock.apply(x, blk, wc, training, info, h, lin, lout, *params)
+    if chain is not None:
+        chain.last = None
     return _Basic.apply(x, blk, wc, training, group, *params)
 
 

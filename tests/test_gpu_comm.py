@@ -48,7 +48,7 @@ def test_emu_comm_sum(gpu):
     m.small_comm_destroy(h)
 
 
-@pytest.mark.parametrize("which", ["layer1.0", "layer1.1", "layer2.0"])
+@pytest.mark.parametrize("which", ["layer1.0", "layer2.0", "layer3.0"])
 @pytest.mark.parametrize("name", ["resnet50", "resnet18"])
 def test_native_executor_syncbn_path(gpu, name, which):
     from simclr_pytorch_distributed_amd.models.executor import ModelRunner
@@ -75,7 +75,12 @@ def test_native_executor_syncbn_path(gpu, name, which):
         info, params = block._block_info(blk)
         flat.zero_grad()
         xi = x.clone().requires_grad_(True)
-        out = block._NativeBlock.apply(xi, blk, wc, True, info, hh, *params)
+        # two chained blocks (the second's final dgrad hands the first its output-BN sums)
+        nxt = getattr(mdl.encoder, lay)[int(idx) + 1]
+        ninfo, nparams = block._block_info(nxt)
+        link = block.BlockLink()
+        mid = block._NativeBlock.apply(xi, blk, wc, True, info, hh, None, link, *params)
+        out = block._NativeBlock.apply(mid, nxt, wc, True, ninfo, hh, link, None, *nparams)
         if dout is None:
             dout = torch.randn_like(out)
         out.backward(dout)

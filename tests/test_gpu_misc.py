@@ -110,4 +110,9 @@ def test_fused_blocks_match_unfused(gpu, name, variant, monkeypatch):
     assert torch.equal(a.encoder.bn1.num_batches_tracked, b.encoder.bn1.num_batches_tracked)
     ga, gb = fa.grad, fb.grad
     rel = ((ga - gb).norm() / gb.norm()).item()
-    assert rel < 1e-3, rel
+    # the executor takes the block-internal BN-backward sums from the dgrad epilogue (a
+    # different fp32 summation order than bn_bwd_reduce): ~1e-7 differences at the first
+    # BN flip bf16 roundings that compound ~10x per block back to the stem at batch 16
+    # (measured 6e-3 on resnet18; bitwise equal with SDX_DGRAD_BNSTAT=0)
+    tol = 2e-2 if variant == "native_exec" else 1e-3
+    assert rel < tol, rel
