@@ -139,8 +139,11 @@ struct Tile {
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
 // BST (DGRAD only): fused BN-backward statistics epilogue (p.bs) — a separate variant so
-// the plain dgrad keeps its register budget.
-template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, bool BST>
+// the plain dgrad keeps its register budget. ONE (LDS-DMA, reduction <= BK): a single
+// K-tile needs no second LDS buffer; the smaller static LDS (one stage or the C tile) lets
+// twice as many blocks share a CU, hiding the load -> MFMA -> store latency of these
+// memory-bound 1x1 layer-1 GEMMs across blocks.
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, bool BST, bool ONE>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
   using T = Tile<MODE, BM, BN, NT>;
@@ -148,7 +151,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves");
   static_assert(T::A_CH >= 1 && T::B_CH >= 1, "tile too small for the thread count");
-  constexpr int LDS = 2 * T::STAGE;
+  constexpr int LDS_C = BM * (BN * 2 + 8);   // C-tile staging (epilogue)
+  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C) : 2 * T::STAGE;
+  static_assert(!ONE || DEPTH == 3, "single-stage variant is LDS-DMA only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const ConvGeom& g = p.g;
@@ -986,16 +991,35 @@ int igemm_ablate() {
   return a;
 }
 
+int igemm_one() {
+  static const int v = [] {
+    const char* e = getenv("SDX_IGEMM_ONE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
-  if constexpr (MODE == MODE_DGRAD) {
-    if (bs) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+  const dim3 g(grid), b(64 * WM * WN);
+  if constexpr (DEPTH == 3 && MODE != MODE_WGRAD) {
+    if (p.Kdim <= BK && igemm_one()) {
+      if (MODE == MODE_DGRAD && bs)
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, MODE == MODE_DGRAD, true>), g, b, 0, s, p);
+      else
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, false, true>), g, b, 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
   }
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+  if constexpr (MODE == MODE_DGRAD) {
+    if (bs) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, true, false>), g, b, 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+  }
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, false, false>), g, b, 0, s, p);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1019,7 +1043,7 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   }
   if constexpr (kDepth2) {
     if (igemm_depth() == 2 && !bs) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2, false, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
