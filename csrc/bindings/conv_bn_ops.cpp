@@ -742,6 +742,15 @@ bool dgrad_bnstat_enabled() {
   return on;
 }
 
+// tensors read by side-stream wgrads, released after the join (no recordStream: blocks
+// return to the allocator in program order instead of behind side-stream events)
+std::vector<torch::Tensor>& side_stash() {
+  static std::vector<torch::Tensor> v;
+  return v;
+}
+
+void side_stash_release() { side_stash().clear(); }
+
 // dW (+)= wgrad(dy, x) into the parameter's gradient sink, on the side stream if given
 void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                 const torch::Tensor& sink, int64_t side) {
@@ -755,8 +764,9 @@ void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int6
   check_hip(hipEventRecord(ev, main), "hipEventRecord");
   check_hip(hipStreamWaitEvent(ss, ev, 0), "hipStreamWaitEvent");
   auto hs = c10::hip::getStreamFromExternal(ss, dy.device().index());
-  c10::hip::HIPCachingAllocator::recordStream(dy.storage().data_ptr(), hs);
-  c10::hip::HIPCachingAllocator::recordStream(x.storage().data_ptr(), hs);
+  // dy / x stay alive until the side stream is joined (ops/streams.py join -> side_stash_release)
+  side_stash().push_back(dy);
+  side_stash().push_back(x);
   c10::hip::HIPStreamGuard guard(hs);
   conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, true, c10::nullopt, c10::nullopt);
 }
@@ -978,6 +988,7 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("inv_b") = pybind11::none(), pybind11::arg("sink_ga") = pybind11::none(),
         pybind11::arg("sink_ba") = pybind11::none(), pybind11::arg("sink_gb") = pybind11::none(),
         pybind11::arg("sink_bb") = pybind11::none());
+  m.def("side_stash_release", &side_stash_release, "drop the tensors kept alive for side-stream wgrads (after join)");
   m.def("conv_dgrad_bnstat", &conv_dgrad_bnstat,
         "dgrad + fused BN-backward statistics of dx (slab [rows][2|3][C] for bn_bwd_coef_slab)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("stride"),

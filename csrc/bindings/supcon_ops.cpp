@@ -72,9 +72,59 @@ std::vector<torch::Tensor> supcon_bwd(torch::Tensor A, torch::Tensor C, torch::T
   return {dA, dC};
 }
 
+// F.normalize(x, dim=1) as one launch: returns (y, row norms)
+std::vector<torch::Tensor> rownorm_fwd(torch::Tensor x, double eps) {
+  check_rows(x, "x");
+  TORCH_CHECK(x.size(1) <= 256, "feature dim must be <= 256");
+  c10::DeviceGuard dg(x.device());
+  auto y = torch::empty_like(x);
+  auto norms = torch::empty({x.size(0)}, x.options());
+  check_hip(launch_rownorm_fwd(x.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (float)eps, y.data_ptr<float>(),
+                               norms.data_ptr<float>(), cur_stream()),
+            "rownorm_fwd");
+  return {y, norms};
+}
+
+torch::Tensor rownorm_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor norms, double eps) {
+  check_rows(dy, "dy");
+  check_rows(y, "y");
+  TORCH_CHECK(dy.sizes() == y.sizes() && norms.is_cuda() && norms.scalar_type() == at::kFloat &&
+                  norms.numel() == y.size(0),
+              "rownorm_bwd shapes");
+  c10::DeviceGuard dg(dy.device());
+  auto dx = torch::empty_like(dy);
+  check_hip(launch_rownorm_bwd(dy.data_ptr<float>(), y.data_ptr<float>(), norms.contiguous().data_ptr<float>(),
+                               (int)dy.size(0), (int)dy.size(1), (float)eps, dx.data_ptr<float>(), cur_stream()),
+            "rownorm_bwd");
+  return dx;
+}
+
+// SEC / L2-reg statistics of un-normalised features (featnorm.hip). mode 0: local sums into
+// `sums` ([2] fp64) only; 1: local sums + finalize; 2: finalize from the given (all-reduced)
+// sums. rec / valid: the record_norm_mean EMA state ([] fp32, updated in place).
+// Returns out [5] = (norm_mean, norm_var, record_norm_mean, loss_sec, loss_l2).
+torch::Tensor norm_stats(torch::Tensor x, int64_t mode, torch::Tensor sums, double n_global, double momentum,
+                         torch::Tensor rec, torch::Tensor valid) {
+  check_rows(x, "x");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.numel() == 2 && sums.is_contiguous(),
+              "sums: [2] float64");
+  TORCH_CHECK(rec.is_cuda() && rec.scalar_type() == at::kFloat && rec.numel() == 1, "rec: float scalar");
+  TORCH_CHECK(valid.is_cuda() && valid.scalar_type() == at::kFloat && valid.numel() == 1, "valid: float scalar");
+  c10::DeviceGuard dg(x.device());
+  auto out = torch::empty({5}, x.options());
+  check_hip(launch_norm_stats(x.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (int)mode, sums.data_ptr<double>(),
+                              n_global, (float)momentum, rec.data_ptr<float>(), valid.data_ptr<float>(),
+                              out.data_ptr<float>(), cur_stream()),
+            "norm_stats");
+  return out;
+}
+
 }  // namespace
 
 void register_supcon(pybind11::module& m) {
+  m.def("rownorm_fwd", &rownorm_fwd, "row L2 normalisation (F.normalize dim=1) -> (y, norms)");
+  m.def("rownorm_bwd", &rownorm_bwd, "gradient of row L2 normalisation");
+  m.def("norm_stats", &norm_stats, "SEC/L2-reg feature-norm statistics + record_norm_mean EMA (one launch)");
   m.def("supcon_fwd", &supcon_fwd, "fused SupCon/NT-Xent forward (row form)");
   m.def("supcon_bwd", &supcon_bwd, "fused SupCon/NT-Xent backward (row form)");
 }

@@ -9,6 +9,13 @@
 // ---- selftest -------------------------------------------------------------------
 hipError_t launch_mfma16_selftest(const void* A, const void* B, float* C, hipStream_t s);
 
+// ---- projection-feature row norms (featnorm.hip) --------------------------------
+hipError_t launch_rownorm_fwd(const float* x, int N, int D, float eps, float* y, float* norms, hipStream_t s);
+hipError_t launch_rownorm_bwd(const float* dy, const float* y, const float* norms, int N, int D, float eps, float* dx,
+                              hipStream_t s);
+hipError_t launch_norm_stats(const float* x, int N, int D, int mode, double* sums, double n_global, float momentum,
+                             float* rec, float* valid, float* out, hipStream_t s);
+
 // ---- fused SupCon / NT-Xent loss (supcon.hip) ---------------------------------
 int supcon_num_splits(int n_own, int n_other);
 hipError_t launch_supcon_fwd(const float* A, const float* C, const int* a_self, const int* a_key,

@@ -210,7 +210,9 @@ class PretrainEngine:
         with ph("loss"):
             loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
             stats = self._norm_terms(feats)
-            loss = loss + stats.pop("extra_loss")
+            extra = stats.pop("extra_loss")
+            if extra is not None:
+                loss = loss + extra
         with ph("backward"):
             self.optimizer.zero_grad()
             loss.backward()
@@ -252,7 +254,9 @@ class PretrainEngine:
         with ph("loss"):
             loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
             stats = self._norm_terms(feats)
-            loss = loss + stats.pop("extra_loss")
+            extra = stats.pop("extra_loss")
+            if extra is not None:
+                loss = loss + extra
             loss.backward()
         gfeat = feats.grad
         self.optimizer.zero_grad()
@@ -311,6 +315,8 @@ class PretrainEngine:
         """SEC / L2-reg regularisers on un-normalised global features (main_supcon.py:295-317).
         The EMA ``record_norm_mean`` and the ramp live in device tensors."""
         opt = self.opt
+        if not (opt.sec or opt.l2reg) and feats.is_cuda and feats.dim() == 2 and _ext.available():
+            return self._norm_stats_native(feats)
         norms = feats.float().norm(dim=1)
         n_global = norms.numel() * self.world
         local = torch.stack([norms.sum(), (norms * norms).sum()])
@@ -336,6 +342,27 @@ class PretrainEngine:
         return {"extra_loss": extra, "norm_mean": norm_mean.detach(), "norm_var": norm_var.detach(),
                 "loss_sec": loss_sec.detach(), "loss_l2reg": loss_l2.detach(),
                 "record_norm_mean": rec.detach().clone()}
+
+    def _norm_stats_native(self, feats):
+        """Logging-only norm statistics (no SEC / L2-reg term in the loss): one launch
+        (csrc/kernels/featnorm.hip) computes them and advances the record_norm_mean EMA.
+        Same semantics as the torch path: global sums are estimated as local·W (no
+        collective) when no regulariser needs the exact global statistics."""
+        m = _ext.require()
+        x = feats.detach().float().contiguous()
+        n_global = float(x.shape[0] * self.world)
+        mom = float(self.opt.norm_momentum)
+        sums = getattr(self, "_ns_sums", None)
+        if sums is None or sums.device != x.device:
+            sums = self._ns_sums = torch.zeros(2, dtype=torch.float64, device=x.device)
+        if self.world > 1:
+            m.norm_stats(x, 0, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
+            sums.mul_(float(self.world))
+            out = m.norm_stats(x, 2, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
+        else:
+            out = m.norm_stats(x, 1, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
+        return {"extra_loss": None, "norm_mean": out[0], "norm_var": out[1], "loss_sec": out[3],
+                "loss_l2reg": out[4], "record_norm_mean": out[2]}
 
     # ------------------------------------------------------------------------------
     def train_epoch(self, epoch: int) -> float:

@@ -54,6 +54,14 @@ def _native_available(t: torch.Tensor) -> bool:
     return contrastive.supported(t)
 
 
+def row_normalize(x: torch.Tensor, backend: str = "auto") -> torch.Tensor:
+    """F.normalize(x, dim=1) — one fused launch each way on GPU (ops/contrastive.py)."""
+    if backend != "torch" and x.is_cuda:
+        from ..ops import contrastive
+        return contrastive.row_normalize(x)
+    return F.normalize(x, dim=1)
+
+
 def supcon_rows_loss(A, C, self_idx, akey, ckey, temperature, base_temperature, scale: float,
                      backend: str = "auto") -> torch.Tensor:
     """``scale * Σ_i ℓ_i`` over the given anchor rows (differentiable w.r.t. A and C)."""
@@ -190,7 +198,7 @@ class DistributedContrastiveLoss(nn.Module):
         w, r = comm.world_size(), comm.rank()
         nv = self.n_views
         b_local = feats.shape[0] // nv
-        n = F.normalize(feats.to(torch.promote_types(feats.dtype, torch.float32)), dim=1)
+        n = row_normalize(feats.to(torch.promote_types(feats.dtype, torch.float32)), self.backend)
         C = comm.all_gather_with_grad(n)
         labels_all = None
         if self.method == "SupCon":

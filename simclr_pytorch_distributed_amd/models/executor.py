@@ -16,6 +16,8 @@ Reference forward: networks/resnet_big.py:57-67 (Bottleneck), 24-35 (BasicBlock)
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -86,6 +88,9 @@ def to_nhwc_input(images: torch.Tensor, c_pad: int = INPUT_CHANNELS_PADDED) -> t
     return x.to(torch.bfloat16).contiguous()
 
 
+FUSED_HEAD = os.environ.get("SDX_FUSED_HEAD", "1") != "0"
+
+
 class ModelRunner:
     """Runs a ``SupConResNet`` (or just its encoder) on the chosen backend.
 
@@ -110,6 +115,9 @@ class ModelRunner:
             from ..ops.weights import ConvWeightCache
             enc = self.model.encoder
             convs = [m for m in enc.modules() if isinstance(m, torch.nn.Conv2d)]
+            head = getattr(self.model, "head", None)
+            if head is not None:
+                convs += [m for m in head.modules() if isinstance(m, torch.nn.Linear)]
             self._wc = ConvWeightCache(convs, self.master, {id(enc.conv1): INPUT_CHANNELS_PADDED})
             self._nbt = [m.num_batches_tracked for m in enc.modules()
                          if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
@@ -144,6 +152,9 @@ class ModelRunner:
 
     def forward(self, x):
         feat = self.encode(x)
+        if self.backend == "native" and self.fused and feat.is_cuda and FUSED_HEAD:
+            from ..ops.head import projection_head
+            return projection_head(feat, self.model.head, self.weight_cache())
         if self.backend == "native" or (x.is_cuda and self.precision == "bf16"):
             return head_forward(self.model.head, feat)
         return self.model.head(feat)

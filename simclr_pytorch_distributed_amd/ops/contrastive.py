@@ -46,6 +46,29 @@ class _SupConRows(torch.autograd.Function):
         return dA.to(ctx.dtypes[0]), dC.to(ctx.dtypes[1]), None, None, None, None, None, None
 
 
+class _RowNorm(torch.autograd.Function):
+    """F.normalize(x, dim=1, eps) on fp32 rows as one launch each way (csrc/kernels/featnorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, eps):
+        y, norms = _ext.require().rownorm_fwd(x.contiguous(), eps)
+        ctx.save_for_backward(y, norms)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, norms = ctx.saved_tensors
+        return _ext.require().rownorm_bwd(dy.contiguous(), y, norms, ctx.eps), None
+
+
+def row_normalize(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """Row L2 normalisation (reference main_supcon.py:283, ``F.normalize(dim=1)``)."""
+    if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.shape[1] <= 256 and _ext.available():
+        return _RowNorm.apply(x, eps)
+    return torch.nn.functional.normalize(x, dim=1, eps=eps)
+
+
 def supcon_rows_loss(A, C, self_idx, akey, ckey, temperature, base_temperature, scale, return_rows=False):
     loss, rows = _SupConRows.apply(A, C, self_idx, akey, ckey, float(temperature), float(base_temperature),
                                    float(scale))

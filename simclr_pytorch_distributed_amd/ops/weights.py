@@ -1,4 +1,5 @@
-"""Per-step bf16 weight cache for the native convolutions.
+"""Per-step bf16 weight cache for the native convolutions (and the projection head's
+Linear layers, treated as 1x1 convs).
 
 The fp32 master conv weights live in the flat parameter buffer (optim/flat.py) in
 channels_last (KRSC) layout. Once per step, ONE kernel (csrc/kernels/wprep.hip) writes
@@ -32,7 +33,8 @@ class ConvWeightCache:
         ok = master is not None
         for cv in convs:
             w = cv.weight
-            K, C, R, S = w.shape
+            # nn.Linear [out][in] = a 1x1 conv: fwd layout W, dgrad layout Wᵀ
+            K, C, R, S = w.shape if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
             Cp = self.cin_pad.get(id(cv), C)
             n_k = K * R * S * Cp
             want_t = Cp == C
@@ -65,7 +67,9 @@ class ConvWeightCache:
         else:
             for cv in self.convs:
                 e = self.entries[id(cv)]
-                w = cv.weight.detach().permute(0, 2, 3, 1).to(torch.bfloat16)     # K R S C
+                w = cv.weight.detach()
+                w = w.view(w.shape[0], w.shape[1], 1, 1) if w.dim() == 2 else w
+                w = w.permute(0, 2, 3, 1).to(torch.bfloat16)     # K R S C
                 fk = self.fwd(cv)
                 fk.zero_()
                 fk[..., : e["C"]].copy_(w)

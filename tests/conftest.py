@@ -20,4 +20,9 @@ def gpu():
         pytest.skip("no GPU")
     from simclr_pytorch_distributed_amd.ops import _ext
     _ext.require()  # native path must load on a GPU box (fail loudly, never fall back)
-    return torch.device("cuda:0")
+    yield torch.device("cuda:0")
+    # drop tensors kept alive for side-stream wgrads by tests that ran a backward
+    # without an optimizer step / reducer join (ops/streams.py)
+    from simclr_pytorch_distributed_amd.ops import streams
+    torch.cuda.synchronize()
+    streams.release()

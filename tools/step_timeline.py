@@ -22,11 +22,16 @@ def main():
     t0, t1 = int(rows[a]["End_Timestamp"]), int(rows[b]["End_Timestamp"])
     busy, cur, gaps = 0, t0, []
     per = defaultdict(float)
+    prev_name = rows[a]["Kernel_Name"]
+    where = []
     for r in rows[a + 1:b + 1]:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         per[r["Kernel_Name"].split("(")[0][:80]] += (e - s) / 1e3
         if s > cur:
             gaps.append((s - cur) / 1e3)
+            where.append(((s - cur) / 1e3, (cur - t0) / 1e3, prev_name[:60], r["Kernel_Name"][:60]))
+        if e > cur:
+            prev_name = r["Kernel_Name"]
         if e <= cur:
             continue
         busy += e - max(s, cur)
@@ -35,6 +40,9 @@ def main():
           f"in {len(gaps)} gaps (largest {max(gaps) if gaps else 0:.1f} us), kernels {b - a}")
     for k, v in sorted(per.items(), key=lambda kv: -kv[1])[:12]:
         print(f"  {v:8.1f} us  {k}")
+    print("largest gaps (us, at us into the step, after -> before):")
+    for g, at, pn, nn in sorted(where, reverse=True)[:15]:
+        print(f"  {g:7.1f} @{at:8.1f}  {pn.split('(')[0]}  ->  {nn.split('(')[0]}")
 
 
 if __name__ == "__main__":
