@@ -4,8 +4,7 @@ single Linear) as ONE autograd node on the native path.
 The GEMMs are plain library GEMMs (hipBLASLt through ``torch.mm``/``addmm``) on the bf16
 weights the per-step weight cache already produced (ops/weights.py: the head's Linear
 layers are cached as 1x1 convs, so no per-step weight casts); weight gradients are
-computed with fp32 output (``mm`` out_dtype) and accumulated straight into the parameter
-sinks. Autograd would otherwise build ~20 nodes for this tiny region (casts, addmm, relu,
+accumulated straight into the parameter sinks. Autograd would otherwise build ~20 nodes for this tiny region (casts, addmm, relu,
 AccumulateGrad), and their host cost leaves the GPU idle between forward and backward.
 Numerics: identical to ``models.executor.head_forward`` (bf16 operands and bias, fp32
 accumulation, ReLU on the bf16 hidden activations).
@@ -20,10 +19,10 @@ _BF = torch.bfloat16
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    try:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    except (RuntimeError, TypeError):   # no mm.dtype for this backend
-        return torch.mm(a.float(), b.float())
+    # bf16 output, accumulated into the fp32 sink by the caller (as autograd's bf16 weight
+    # grad + AccumulateGrad did): ``mm(out_dtype=fp32)`` measured ~160 us of host time per
+    # call on this stack, which left the GPU idle in the head region
+    return torch.mm(a, b)
 
 
 class _MLPHead(torch.autograd.Function):
