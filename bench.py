@@ -115,12 +115,13 @@ def main():
     loss = float(st["loss_local"].item())
     ms = dt / a.steps * 1e3
     value = global_batch * a.steps / dt
+    d_in = {"resnet18": 512, "resnet34": 512}.get(a.model, 2048)
     if comm.rank() == 0:
         print(json.dumps({
             "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"model": f"{a.model} (CIFAR stem) + MLP head 2048-2048-128, SimCLR tau=0.5",
+            "config": {"model": f"{a.model} (CIFAR stem) + MLP head {d_in}-{d_in}-128, SimCLR tau=0.5",
                        "global_batch": global_batch, "per_gpu_batch": a.per_gpu_batch, "views": 2,
                        "image_size": 32, "seq_len": None,
                        "parallelism": f"dp{n}" + ("+syncbn" if n > 1 and not a.no_syncbn else ""),

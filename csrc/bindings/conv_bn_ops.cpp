@@ -250,8 +250,13 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     splits = std::max<int64_t>(1, 512 / tiles);
     const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
     splits = std::min(splits, max_splits);
-    // bound the fp32 partial slab to ~64 MiB
-    splits = std::min<int64_t>(splits, std::max<int64_t>(1, (16LL << 20) / (M * Ncol)));
+    // bound the fp32 partial slab to ~64 MiB, and to ~16 MiB / 256 splits for 1x1 GEMMs with
+    // a small output (M*Ncol <= 64K: the layer-1/2 pointwise convs), where the slab round
+    // trip outweighs the extra splits' parallelism (profiles/wgrad_sweep_r1.txt: 83 -> 67 us
+    // on the 256x64 layer-1 GEMMs; the 3x3 and larger GEMMs keep more splits)
+    const bool small_1x1 = R == 1 && S == 1 && M * Ncol <= 65536;
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, (small_1x1 ? (4LL << 20) : (16LL << 20)) / (M * Ncol)));
+    if (small_1x1) splits = std::min<int64_t>(splits, 256);
   }
   splits = conv_wgrad_splits(g, (int)cfg, (int)splits);
   torch::Tensor dw;

@@ -117,6 +117,22 @@ __device__ __forceinline__ uint4 bnrelu8(uint4 v, const float (&s)[8], const flo
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt at their maxima); gfx9 encoding: vmcnt in
+// bits [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+}
+
+// raw workgroup barrier: this wave's LDS reads complete first; LDS-DMA stays in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
   const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
@@ -152,8 +168,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves");
   static_assert(T::A_CH >= 1 && T::B_CH >= 1, "tile too small for the thread count");
   constexpr int LDS_C = BM * (BN * 2 + 8);   // C-tile staging (epilogue)
-  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C) : 2 * T::STAGE;
+  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C) : (DEPTH == 4 ? 3 : 2) * T::STAGE;
   static_assert(!ONE || DEPTH == 3, "single-stage variant is LDS-DMA only");
+  static_assert(DEPTH != 4 || MODE != MODE_WGRAD, "LDS-DMA ring is FWD/DGRAD only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const ConvGeom& g = p.g;
@@ -179,7 +196,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   // K-inner operands. Register staging: thread owns chunk column ch = tid % 8 and rows
   // tid/8 + (NT/8)*i. LDS-DMA: instruction i of wave w fills rows 8*(w*CH + i) .. +7 (1 KiB),
   // lane L row +L/8 at physical chunk L%8, i.e. logical chunk (L&7)^(L>>3).
-  constexpr bool GL = DEPTH == 3;
+  constexpr bool GL = DEPTH >= 3;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
   const int kin_ch = GL ? ((lane & 7) ^ ((lane >> 3) & 7)) : (tid & 7);
   const int kin_row0 = tid >> 3;
@@ -633,7 +650,25 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
   // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
   // issued a whole K-tile earlier (load latency covered by two tiles of MFMA work).
-  if (DEPTH == 3) {
+  if (DEPTH == 4) {
+    // 3-buffer LDS-DMA ring: tile k+2's DMA is issued while tile k computes. The counted
+    // vmcnt before each raw barrier retires only tile k; tile k+1 stays in flight across
+    // it (a __syncthreads() would drain every DMA: its fence waits vmcnt(0)). The buffer
+    // refilled after the barrier held tile k-1, whose reads every wave finished before
+    // arriving there. Past-the-end tiles load the zero page, so any nk is safe.
+    constexpr int NL = T::A_CH + T::B_CH;   // global_load_lds per wave per tile
+    issue_glds(k_begin, 0);
+    issue_glds(k_begin + BK, 1);
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) vm_wait<NL>(); else vm_wait<0>();
+      lds_barrier();
+      if (kt + 2 < nk) issue_glds(k_begin + (kt + 2) * BK, buf == 0 ? 2 : buf - 1);
+      compute(buf);
+      buf = buf == 2 ? 0 : buf + 1;
+    }
+    __syncthreads();
+  } else if (DEPTH == 3) {
     // the DMA of tile k+1 overlaps the MFMAs of tile k; the barrier's vmcnt(0) lands it
     if (nk > 0) issue_glds(k_begin, 0);
     __syncthreads();
@@ -991,6 +1026,15 @@ int igemm_ablate() {
   return a;
 }
 
+// 3-buffer LDS-DMA ring for FWD/DGRAD GEMMs of more than two K-tiles (SDX_IGEMM_RING=1)
+int igemm_ring() {
+  static const int v = [] {
+    const char* e = getenv("SDX_IGEMM_RING");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int igemm_one() {
   static const int v = [] {
     const char* e = getenv("SDX_IGEMM_ONE");
@@ -1038,6 +1082,9 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
     // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
     // (SDX_IGEMM_GLDS=2 enables it there too)
     if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
+      if constexpr (MODE != MODE_WGRAD) {
+        if (igemm_ring() && p.Kdim > 2 * BK) return launch_k<MODE, BM, BN, WM, WN, 4>(bs, grid, p, s);
+      }
       return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
     }
   }

@@ -72,6 +72,12 @@ class PretrainEngine:
         self.opt = opt
         rank, local_rank, world, dev = comm.init_distributed(opt.dist_backend, getattr(opt, "comm_timeout", 600.0), device=device)
         self.rank, self.world, self.device = rank, world, dev
+        self.stream = None
+        if dev.type == "cuda" and os.environ.get("SDX_STREAM_PRIO", "0") != "0":
+            # the whole step on a high-priority stream: the critical path (forward, BN,
+            # dgrad chain) is dispatched ahead of the default-priority wgrad side stream
+            self.stream = torch.cuda.Stream(device=dev, priority=-1)
+            torch.cuda.set_stream(self.stream)
         if opt.ngpu != world and world > 1:
             logging.warning(f"--ngpu {opt.ngpu} != launcher WORLD_SIZE {world}; using {world}")
         opt.world_size = world

@@ -1,0 +1,39 @@
+"""bench.py driver contract on CPU: 2 ranks under torch.distributed.run (gloo), the torch
+backend and a small model. Checks the single JSON line rank 0 prints (keys, whole-job
+value, weak scaling of the global batch) — the same code path the 8-GPU scaling run takes,
+minus the GPU kernels."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_json_contract(tmp_path):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "torch", "--model", "resnet18",
+           "--per_gpu_batch", "4"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    c = d["config"]
+    assert c["global_batch"] == 8 and c["per_gpu_batch"] == 4 and c["parallelism"] == "dp2+syncbn"
+    # value = whole-job images/s = global batch x steps / time
+    assert abs(d["value"] - 8 * 1e3 / d["ms_per_step"]) / d["value"] < 0.01
