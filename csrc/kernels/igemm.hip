@@ -101,8 +101,12 @@ __device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_c
 // A predicated load makes hipcc branch around it and drain the whole load queue
 // (vmcnt(0)) before the LDS write, which defeats any prefetch depth.
 __device__ __attribute__((aligned(16))) uint16_t g_zero16[8];
-__device__ __forceinline__ uint4 ld16_or_zero(const uint16_t* p, bool ok) {
-  return ld16(ok ? p : g_zero16);
+// g_zero16's address in an SGPR pair the compiler cannot rematerialise: otherwise it re-runs
+// s_getpc + a GOT s_load + s_waitcnt lgkmcnt(0) before every zero-page select of the K loop
+__device__ __forceinline__ const uint16_t* opaque_zero() {
+  const uint16_t* z = g_zero16;
+  asm volatile("" : "+s"(z));
+  return z;
 }
 
 // relu(x·s + t) on 8 packed bf16 channels (fp32 math, one rounding: same as bn_apply)
@@ -174,6 +178,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const ConvGeom& g = p.g;
+  const uint16_t* const zp = opaque_zero();
+  auto ld16_or_zero = [&](const uint16_t* q, bool ok) { return ld16(ok ? q : zp); };
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h = lane >> 4, c = lane & 15;
   const int wm = wv / WN, wn = wv % WN;
@@ -206,6 +212,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
   // tap; DGRAD: dy coordinate of tap (r0, s0))
   int a_base[T::A_CH], a_y[T::A_CH], a_x[T::A_CH];
+  int a_rb[T::A_CH];   // LDS-DMA path: row base incl. its spatial origin (0 for rows past M)
   int b_off[T::B_CH];
   // k decode of this thread's chunk: k = kc + cdim*(ks + ns*kr)
   int kc = 0, ks = 0, kr = 0;
@@ -235,6 +242,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         a_x[i] = -(1 << 28);
         a_base[i] = 0;
       }
+    }
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i) {
+      const bool row_ok = a_y[i] > -(1 << 27);
+      a_rb[i] = !row_ok ? 0 : (MODE == MODE_FWD ? a_base[i] : a_base[i] + (a_y[i] * g.Q + a_x[i]) * g.K);
     }
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
@@ -446,7 +458,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         const int kk = k0 + row, co = m0 + ch * 8;
         const bool ok = kk < k_end && co < p.M;
         SDX_DCHECK(!ok || (long)kk * g.K + co + 8 <= p.a_elems);
-        const uint16_t* src = ok ? p.a + kk * g.K + co : g_zero16;
+        const uint16_t* src = ok ? p.a + kk * g.K + co : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sa + (wvu * T::A_CH + i) * 1024),
                                          16, 0, 0);
@@ -467,7 +479,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
           off = ((n * g.H + yy) * g.W + xx) * g.C + gb_c[i];
         }
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.b_elems));
-        const uint16_t* src = ok ? p.b + off : g_zero16;
+        const uint16_t* src = ok ? p.b + off : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + (wvu * T::B_CH + i) * 1024),
                                          16, 0, 0);
@@ -485,7 +497,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         const bool ok = kok && ((vmask[i] >> tap) & 1u);
         const int off = rbase[i] + toff + lane_c;
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
-        const uint16_t* src = ok ? p.a + off : g_zero16;
+        const uint16_t* src = ok ? p.a + off : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -494,7 +506,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       for (int i = 0; i < T::B_CH; ++i) {
         const bool ok = kok && b_off[i] >= 0;
         SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-        const uint16_t* src = ok ? p.b + b_off[i] + k : g_zero16;
+        const uint16_t* src = ok ? p.b + b_off[i] + k : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -506,26 +518,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       }
       return;
     }
+    // the tap offset of this thread's chunk column is the same for every row it stages:
+    // one multiply per K-tile, then per row a bounds test and an add (no 1x1 special case:
+    // its taps stay (0, 0))
+    const int toff = (MODE == MODE_FWD) ? (kr * g.W + ks) * g.C + kc : kc - (kr * g.Q + ks) * g.K;
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
       bool ok;
-      int off;
-      if (MODE == MODE_FWD) {
-        if (is1x1) {
-          ok = kok && a_y[i] >= 0;
-          off = a_base[i] + kc;
-        } else {
-          const int yy = a_y[i] + kr, xx = a_x[i] + ks;
-          ok = kok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
-          off = a_base[i] + (kr * g.W + ks) * g.C + kc;
-        }
-      } else {
-        const int ty = a_y[i] - kr, tx = a_x[i] - ks;
-        ok = kok && (unsigned)ty < (unsigned)g.P && (unsigned)tx < (unsigned)g.Q;
-        off = a_base[i] + (ty * g.Q + tx) * g.K + kc;
-      }
+      if (MODE == MODE_FWD)
+        ok = kok && (unsigned)(a_y[i] + kr) < (unsigned)g.H && (unsigned)(a_x[i] + ks) < (unsigned)g.W;
+      else
+        ok = kok && (unsigned)(a_y[i] - kr) < (unsigned)g.P && (unsigned)(a_x[i] - ks) < (unsigned)g.Q;
+      const int off = a_rb[i] + toff;
       SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
-      const uint16_t* src = ok ? p.a + off : g_zero16;
+      const uint16_t* src = ok ? p.a + off : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
                                        16, 0, 0);
@@ -534,7 +540,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     for (int i = 0; i < T::B_CH; ++i) {
       const bool ok = kok && b_off[i] >= 0;
       SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-      const uint16_t* src = ok ? p.b + b_off[i] + k : g_zero16;
+      const uint16_t* src = ok ? p.b + b_off[i] + k : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                        16, 0, 0);

@@ -116,3 +116,24 @@ def test_fused_blocks_match_unfused(gpu, name, variant, monkeypatch):
     # (measured 6e-3 on resnet18; bitwise equal with SDX_DGRAD_BNSTAT=0)
     tol = 2e-2 if variant == "native_exec" else 1e-3
     assert rel < tol, rel
+
+
+def test_native_engine_step_imagenet_supcon_lars(gpu, tmp_path):
+    """SURVEY config 5 in miniature: SupCon, ImageNet stem (7x7/2 + max-pool) at 224x224,
+    LARS, native backend — three steps: finite loss, weights move and stay finite."""
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    opt = parse_pretrain(["--batch_size", "16", "--synthetic", "--synthetic_size", "64", "--work_dir", str(tmp_path),
+                          "--model", "resnet50", "--backend", "native", "--method", "SupCon", "--stem", "imagenet",
+                          "--size", "224", "--optimizer", "lars", "--learning_rate", "0.3"], make_dirs=False)
+    eng = PretrainEngine(opt)
+    assert eng.backend == "native"
+    idx = torch.arange(16, device=gpu)
+    w0 = eng.flat.flat.clone()
+    losses = []
+    for _ in range(3):
+        st = eng.train_step(idx, 1, 0, 10)
+        losses.append(float(st["loss_local"].item()))
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert not torch.equal(w0, eng.flat.flat)
+    assert torch.isfinite(eng.flat.flat).all().item()
