@@ -103,8 +103,9 @@ __device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_c
 __device__ __attribute__((aligned(16))) uint16_t g_zero16[8];
 // g_zero16's address in an SGPR pair the compiler cannot rematerialise: otherwise it re-runs
 // s_getpc + a GOT s_load + s_waitcnt lgkmcnt(0) before every zero-page select of the K loop
-__device__ __forceinline__ const uint16_t* opaque_zero() {
-  const uint16_t* z = g_zero16;
+typedef const __attribute__((address_space(1))) uint16_t* gptr16;
+__device__ __forceinline__ gptr16 opaque_zero() {
+  gptr16 z = (gptr16)g_zero16;
   asm volatile("" : "+s"(z));
   return z;
 }
@@ -178,8 +179,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const ConvGeom& g = p.g;
-  const uint16_t* const zp = opaque_zero();
-  auto ld16_or_zero = [&](const uint16_t* q, bool ok) { return ld16(ok ? q : zp); };
+  const gptr16 zp = opaque_zero();
+  // the address-space cast keeps these global_load (the opaque zero pointer is generic: a
+  // select with it would otherwise become a flat load, counted by lgkmcnt as well)
+  auto ld16_or_zero = [&](const uint16_t* q, bool ok) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(ok ? (gptr16)q : zp);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h = lane >> 4, c = lane & 15;
   const int wm = wv / WN, wn = wv % WN;
@@ -458,7 +465,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         const int kk = k0 + row, co = m0 + ch * 8;
         const bool ok = kk < k_end && co < p.M;
         SDX_DCHECK(!ok || (long)kk * g.K + co + 8 <= p.a_elems);
-        const uint16_t* src = ok ? p.a + kk * g.K + co : zp;
+        const gptr16 src = ok ? (gptr16)(p.a + kk * g.K + co) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sa + (wvu * T::A_CH + i) * 1024),
                                          16, 0, 0);
@@ -479,7 +486,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
           off = ((n * g.H + yy) * g.W + xx) * g.C + gb_c[i];
         }
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.b_elems));
-        const uint16_t* src = ok ? p.b + off : zp;
+        const gptr16 src = ok ? (gptr16)(p.b + off) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + (wvu * T::B_CH + i) * 1024),
                                          16, 0, 0);
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         const bool ok = kok && ((vmask[i] >> tap) & 1u);
         const int off = rbase[i] + toff + lane_c;
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
-        const uint16_t* src = ok ? p.a + off : zp;
+        const gptr16 src = ok ? (gptr16)(p.a + off) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -506,7 +513,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       for (int i = 0; i < T::B_CH; ++i) {
         const bool ok = kok && b_off[i] >= 0;
         SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-        const uint16_t* src = ok ? p.b + b_off[i] + k : zp;
+        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         ok = kok && (unsigned)(a_y[i] - kr) < (unsigned)g.P && (unsigned)(a_x[i] - ks) < (unsigned)g.Q;
       const int off = a_rb[i] + toff;
       SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
-      const uint16_t* src = ok ? p.a + off : zp;
+      const gptr16 src = ok ? (gptr16)(p.a + off) : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
                                        16, 0, 0);
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     for (int i = 0; i < T::B_CH; ++i) {
       const bool ok = kok && b_off[i] >= 0;
       SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-      const uint16_t* src = ok ? p.b + b_off[i] + k : zp;
+      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                        16, 0, 0);
