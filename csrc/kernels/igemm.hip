@@ -39,6 +39,9 @@ constexpr int BK = 64;
 #ifndef SDX_FAST_TAPS
 #define SDX_FAST_TAPS 0
 #endif
+#ifndef SDX_PRIO_HALF
+#define SDX_PRIO_HALF 1
+#endif
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
@@ -659,6 +662,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[u][j], af[u][i], acc[i][j], 0, 0, 0);
   };
 
+  // 8-wave blocks: the second-dispatched half loses VALU/issue arbitration to the older half
+  // on every segment; one static priority raise for it (no per-cluster flips). SDX_PRIO_HALF
+  if (SDX_PRIO_HALF && NT == 512 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   // K loop: two LDS buffers, one barrier per K-tile. DEPTH 1: the loads of tile k+1 are in
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
   // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
