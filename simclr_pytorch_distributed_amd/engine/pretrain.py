@@ -159,8 +159,20 @@ class PretrainEngine:
             except Exception as e:  # noqa: BLE001
                 logging.warning(f"one-shot xGMI all-reduce unavailable ({e}); using RCCL")
         if comm.backend() == "nccl" and os.environ.get("SDX_NATIVE_SYNCBN", "1") != "0":
-            comm.set_native_small_comm(None, comm.create_rccl_small_comm(None))
-            logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
+            handle, err = 0, None
+            try:
+                handle = comm.create_rccl_small_comm(None)
+            except Exception as e:  # noqa: BLE001
+                err = e
+            # every rank must agree, or the BN collectives would be mismatched across ranks
+            ok = torch.tensor([0.0 if err is not None else 1.0], device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() == 1.0:
+                comm.set_native_small_comm(None, handle)
+                logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
+            else:
+                logging.warning(f"dedicated RCCL communicator unavailable on some rank ({err}); "
+                                "SyncBN statistics use the process-group all-reduce")
 
     def _resume(self, path):
         st = ckpt_mod.load_checkpoint(path)
