@@ -243,6 +243,14 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
               "wgrad geometry mismatch");
   c10::DeviceGuard dg(x.device());
   const int64_t M = g.K, Ncol = (int64_t)R * S * g.C, Kd = (int64_t)g.N * g.P * g.Q;
+  // 64-output-channel GEMMs with a wide reduction side (layer-1 3x3: 64 x 576): the 64x256
+  // tile (four 64x64 wave tiles) beats the exact-fit 64x64 one despite its padding, at
+  // ~512 blocks (tools/wgrad_split_probe.py: 145 -> 124 us)
+  static const bool wide64 = [] {
+    const char* e = getenv("SDX_WGRAD_WIDE64");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (wide64 && cfg < 0 && splits <= 0 && M <= 64 && Ncol >= 512) cfg = 2;
   if (cfg < 0) cfg = auto_cfg(M, Ncol);
   if (splits <= 0) {
     const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
