@@ -112,7 +112,7 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
 // bs (optional): fused BN-backward statistics; its slab must hold conv_dgrad_slab_rows rows
 torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                               int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
-                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs) {
+                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
   TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
@@ -135,9 +135,19 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     dx = torch::empty({g.N, g.H, g.W, g.C}, dy.options());
   }
   const void* add = nullptr;
+  TORCH_CHECK(addend_sub >= 0, "addend_sub");
   if (addend.has_value()) {
     check_bf16_nhwc(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
+    if (addend_sub > 1) {
+      // compact addend on the stride-s subgrid (h, w ≡ 0 mod s)
+      const int64_t s_ = addend_sub;
+      TORCH_CHECK(addend->size(0) == g.N && addend->size(1) == (g.H + s_ - 1) / s_ &&
+                      addend->size(2) == (g.W + s_ - 1) / s_ && addend->size(3) == g.C,
+                  "compact addend shape [N, ceil(H/s), ceil(W/s), C]");
+      TORCH_CHECK(!addend_mask.has_value(), "addend_mask is not supported with a compact addend");
+    } else {
+      TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
+    }
     add = addend->data_ptr();
   }
   const void* amask = nullptr;
@@ -151,7 +161,7 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   if (bs) bs->row0 = 0;
   if (stride == 1) {
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                      cur_stream(), amask, bs),
+                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0),
               "conv_dgrad");
     return dx;
   }
@@ -166,7 +176,7 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
       else
         wc = wt;   // no taps: the kernel writes zeros and never reads B
       check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                        cur_stream(), amask, bs),
+                                        cur_stream(), amask, bs, add ? (int)addend_sub : 0),
                 "conv_dgrad(class)");
       if (bs) bs->row0 += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
     }
@@ -175,8 +185,8 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
 
 torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                          int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
-                         c10::optional<torch::Tensor> addend_mask) {
-  return conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, nullptr);
+                         c10::optional<torch::Tensor> addend_mask, int64_t addend_sub = 0) {
+  return conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, nullptr, addend_sub);
 }
 
 // dgrad + fused BN-backward statistics of dx for the BN whose pre-BN tensor is ya (and yb,
@@ -185,7 +195,7 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
 std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W,
                                              int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
                                              OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
-                                             OptT mask_bits, OptT msc, OptT msh) {
+                                             OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0) {
   check_bf16_nhwc(ya, "ya");
   const int64_t C = wt.size(0);
   TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
@@ -225,7 +235,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
   const int ns = yb.has_value() ? 3 : 2;
   auto slab = torch::empty({rows, ns, C}, dy.options().dtype(at::kFloat));
   bs.slab = slab.data_ptr<float>();
-  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs);
+  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs, addend_sub);
   return {dx, slab};
 }
 
@@ -747,6 +757,14 @@ std::vector<torch::Tensor> bn_bwd_coef_slab(int64_t comm, torch::Tensor slab, do
   return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
 }
 
+bool sub_addend_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SDX_SUB_ADDEND");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 bool dgrad_bnstat_enabled() {
   static const bool on = [] {
     const char* e = getenv("SDX_DGRAD_BNSTAT");
@@ -939,20 +957,29 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   // the final dgrad (the one that stores dx) optionally emits the previous block's output-BN sums
   const bool want_prev = dgrad_bnstat_enabled() && prev.size() == 5 && prev[4].defined() && prev[4].numel() > 0;
   torch::Tensor prev_slab;
-  auto last_dgrad = [&](OptT o, OptT add, OptT amask) -> torch::Tensor {
-    if (!want_prev) return conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, o, add, amask);
+  auto last_dgrad = [&](OptT o, OptT add, OptT amask, int64_t asub = 0) -> torch::Tensor {
+    if (!want_prev) return conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, asub);
     const bool two = prev[2].defined() && prev[2].numel() > 0;
     auto r = conv_dgrad_bnstat(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, prev[0], prev[1],
                                two ? OptT(prev[2]) : OptT(), two ? OptT(prev[3]) : OptT(), prev[4], c10::nullopt,
-                               c10::nullopt);
+                               c10::nullopt, asub);
     prev_slab = r[1];
     return r[0];
   };
   torch::Tensor dx;
   if (proj) {
     side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);
-    dx = conv_dgrad(dys, wt[nconv], H, W, stride, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt);
-    dx = last_dgrad(dx, dx, c10::nullopt);
+    if (stride > 1 && sub_addend_enabled()) {
+      // the strided 1x1 shortcut's data gradient lives on the stride-s subgrid only: compute
+      // it compactly (a stride-1 1x1 dgrad on the P x Q grid) and let the final dgrad add it
+      // there — no zero sub-pixel classes written, no zeros re-read as the addend
+      auto dxs = conv_dgrad(dys, wt[nconv], dys.size(1), dys.size(2), 1, 0, -1, c10::nullopt, c10::nullopt,
+                            c10::nullopt, 0);
+      dx = last_dgrad(c10::nullopt, dxs, c10::nullopt, stride);
+    } else {
+      dx = conv_dgrad(dys, wt[nconv], H, W, stride, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt, 0);
+      dx = last_dgrad(dx, dx, c10::nullopt);
+    }
   } else if (dz.defined()) {
     dx = last_dgrad(c10::nullopt, dz, c10::nullopt);
   } else {
@@ -971,7 +998,8 @@ void register_conv_bn(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv data gradient (strided: sub-pixel classes)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none());
+        pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none(),
+        pybind11::arg("addend_sub") = 0);
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K slab)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("splits") = 0, pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
@@ -1009,7 +1037,8 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none(),
         pybind11::arg("ya"), pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(),
         pybind11::arg("mb") = pybind11::none(), pybind11::arg("mask_bits") = pybind11::none(),
-        pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none());
+        pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none(),
+        pybind11::arg("addend_sub") = 0);
   m.def("bn_bwd_coef_slab", &bn_bwd_coef_slab, "BN-backward coefficients (+dγ/dβ into sinks) from a dgrad stat slab",
         pybind11::arg("comm"), pybind11::arg("slab"), pybind11::arg("count"), pybind11::arg("g_a"),
         pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),

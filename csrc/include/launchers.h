@@ -60,7 +60,7 @@ void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* 
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
-                                   const BnBwdStat* bstat = nullptr);
+                                   const BnBwdStat* bstat = nullptr, int addend_sub = 0);
 // M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
 int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);

@@ -53,6 +53,10 @@ struct IgemmParams {
   void* out;           // FWD/DGRAD: bf16 rows of Ncol; WGRAD: fp32 partial slab [splits][M][Ncol]
   float* stats;        // FWD: [m_tiles][2][Ncol] (Σy, Σy²) or nullptr
   const uint16_t* addend;   // DGRAD: optional bf16 tensor (same layout as out) added in the epilogue
+  // DGRAD: addend_sub = s > 1: the addend is COMPACT, [N][ceil(H/s)][ceil(W/s)][C], and is
+  // added only at output pixels (h, w) with h % s == w % s == 0 (a strided 1x1 shortcut's
+  // data gradient, which is zero everywhere else)
+  int addend_sub;
   // optional fused BatchNorm+ReLU on the activation operand as it is loaded (FWD: A = x,
   // WGRAD: B = x): x' = max(x·in_scale[c] + in_shift[c], 0); padding taps stay exactly 0
   const float* in_scale;
@@ -778,11 +782,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr bool bst = MODE == MODE_DGRAD && BST;
   const int my_ch = tid % CPR, my_col = n0 + my_ch * 8;
   int eo[ITER];   // output element offset of each chunk (-1: outside the tensor)
+  int ea[ITER];   // addend element offset (-1: no addend there)
+  const int asub = (MODE == MODE_DGRAD) ? p.addend_sub : 0;
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
     const int row = (tid + it * NT) / CPR;
     const int m = m0 + row;
-    int o = -1;
+    int o = -1, oa = -1;
     if (m < p.M && my_col < p.Ncol) {
       int orow = m;
       if (MODE == MODE_DGRAD && g.stride != 1) {
@@ -792,8 +798,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         orow = (n * g.H + yy * g.stride + p.ph) * g.W + xx * g.stride + p.pw;
       }
       o = orow * p.Ncol + my_col;
+      oa = o;
+      if (asub > 1) {
+        const int hw = g.H * g.W;
+        const int n = orow / hw, rem = orow - n * hw;
+        const int hh = rem / g.W, ww = rem - hh * g.W;
+        const int Hs = (g.H + asub - 1) / asub, Ws = (g.W + asub - 1) / asub;
+        oa = (hh % asub == 0 && ww % asub == 0) ? ((n * Hs + hh / asub) * Ws + ww / asub) * p.Ncol + my_col : -1;
+      }
     }
     eo[it] = o;
+    ea[it] = oa;
   }
   uint4 pf_add[PF], pf_ya[PF], pf_yb[PF];
   uint32_t pf_am[PF], pf_bm[PF];
@@ -804,7 +819,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     if (MODE == MODE_DGRAD && has_add) {
       // (the zero page, not a private zero: a select between a global and a private
       // address would turn the load into a flat load and spill the zero to scratch)
-      pf_add[sl] = ld16_or_zero(p.addend + (ok ? o : 0), ok);
+      const int oa = ea[it];
+      pf_add[sl] = ld16_or_zero(p.addend + (oa >= 0 ? oa : 0), oa >= 0);
       pf_am[sl] = (ok && p.addend_mask != nullptr) ? (uint32_t)p.addend_mask[o >> 3] : 0xffu;
     }
     if (MODE == MODE_DGRAD && bst) {
@@ -1181,8 +1197,9 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
-                                   const BnBwdStat* bstat) {
+                                   const BnBwdStat* bstat, int addend_sub) {
   IgemmParams p{};
+  p.addend_sub = addend_sub;
   if (bstat != nullptr) p.bs = *bstat;
   p.addend_mask = (const uint8_t*)addend_mask;
   p.g = g;

@@ -247,3 +247,30 @@ def test_dgrad_bn_stats_two_sets_with_addend(gpu):
     assert ((s[0] - d.sum(0)).abs() / sc).max() < 1e-4
     assert ((s[1] - (d * (ya.double().reshape(-1, C) - ma.double())).sum(0)).abs() / (4 * sc)).max() < 1e-4
     assert ((s[2] - (d * (yb.double().reshape(-1, C) - mb.double())).sum(0)).abs() / (4 * sc)).max() < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 8, 64, 128), (2, 9, 7, 32, 64)])
+def test_dgrad_compact_subgrid_addend(gpu, shape):
+    """conv_dgrad(addend=compact, addend_sub=2) == conv_dgrad(addend=the strided 1x1 shortcut's
+    full dgrad): the shortcut gradient is added only at even (h, w), read from a compact
+    [N, ceil(H/2), ceil(W/2), C] tensor; also through the BN-statistics variant."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    torch.manual_seed(11)
+    N, H, W, C, K = shape
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dy1 = torch.randn(N, H, W, K, device=gpu).bfloat16()          # c1 (1x1, stride 1) output grad
+    wt1 = (torch.randn(C, 1, 1, K, device=gpu) * 0.05).bfloat16()
+    dys = torch.randn(N, P, Q, 2 * K, device=gpu).bfloat16()      # shortcut (1x1, stride 2) output grad
+    wts = (torch.randn(C, 1, 1, 2 * K, device=gpu) * 0.05).bfloat16()
+    full = m.conv_dgrad(dys, wts, H, W, 2, 0)
+    compact = m.conv_dgrad(dys, wts, P, Q, 1, 0)
+    assert torch.equal(full[:, ::2, ::2, :], compact)
+    ref = m.conv_dgrad(dy1, wt1, H, W, 1, 0, -1, None, full)
+    out = m.conv_dgrad(dy1, wt1, H, W, 1, 0, -1, None, compact, None, 2)
+    assert torch.equal(out, ref)
+    y = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    mu = torch.zeros(C, device=gpu)
+    r_ref = m.conv_dgrad_bnstat(dy1, wt1, H, W, 1, 0, -1, None, full, None, y, mu)
+    r = m.conv_dgrad_bnstat(dy1, wt1, H, W, 1, 0, -1, None, compact, None, y, mu, addend_sub=2)
+    assert torch.equal(r[0], r_ref[0]) and torch.allclose(r[1], r_ref[1], rtol=1e-5, atol=1e-5)
