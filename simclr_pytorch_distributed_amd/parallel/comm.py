@@ -50,7 +50,10 @@ def init_distributed(backend_name: str = "auto", timeout_s: float = 600.0, devic
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available()
     if device is None:
-        device = torch.device(f"cuda:{local}") if use_cuda else torch.device("cpu")
+        # more local ranks than visible GPUs (a multi-rank rehearsal on a 1-GPU box):
+        # ranks share devices round-robin instead of failing on a missing ordinal
+        device = torch.device(f"cuda:{local % max(torch.cuda.device_count(), 1)}") if use_cuda \
+            else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if world > 1 and not is_dist():

@@ -1,0 +1,21 @@
+# Rehearse the driver's N>1 bench launch (torch.distributed.run, one rank per "GPU") on a
+# 1-GPU box: both ranks share cuda:0 (comm.init_distributed maps local ranks round-robin).
+# First the production path (RCCL process group + RCCL SyncBN communicator); if RCCL
+# refuses two ranks on one device (plain error, exit 1), the gloo process group instead.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+O=gpurun_out/multirank
+mkdir -p $O
+run() {  # $1 = tag, rest = extra bench args
+  tag=$1; shift
+  timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29561 bench.py --gpus 2 --steps 10 --warmup 3 "$@" > $O/$tag.log 2>&1
+}
+run nccl; rc=$?
+echo "nccl rc=$rc"; grep '"metric"' $O/nccl.log || tail -15 $O/nccl.log
+[ $rc -eq 0 ] && exit 0
+[ $rc -ne 1 ] && exit $rc
+run gloo --dist_backend gloo; rc=$?
+echo "gloo rc=$rc"; grep '"metric"' $O/gloo.log || tail -15 $O/gloo.log
+exit $rc
