@@ -6,25 +6,52 @@
 // is a handle the executor (conv_bn_ops.cpp block_fwd / block_bwd) calls directly on the
 // compute stream, with no Python or c10d work queue in between:
 //
-//   kind RCCL  — a dedicated RCCL communicator (ncclCommInitRank from a unique id the
-//                Python side broadcasts once through torch.distributed); ncclAllReduce
-//                in place on the current stream. Separate from torch's communicators, so
-//                the gradient buckets (their own process group / stream) never queue in
-//                front of a SyncBN statistic.
+//   kind RCCL  — a dedicated RCCL communicator (ncclCommInitRankConfig from a unique id
+//                the Python side broadcasts once through torch.distributed); ncclAllReduce
+//                in place on the current stream.
 //   kind XGMI  — a one-shot IPC arena of xgmi_ops.cpp (direct peer stores + epoch flags).
 //   kind EMU   — W virtual ranks holding identical data in ONE process (tests): the sum is
 //                x·W, so every SyncBN code path of the executor runs on a single GPU and
-//                must reproduce the single-process result (statistics exactly, dγ/dβ ×W).
+//                must reproduce the single-process result.
+//
+// Failure handling. The RCCL communicator is created NON-blocking
+// (config.blocking = 0): initialisation is polled against a deadline and aborted on
+// expiry, so a peer that never joins raises here instead of hanging. Every communicator
+// of >1 rank is watched by ONE host watchdog thread: after a collective is enqueued the
+// issuing thread moves a HIP event behind it (throttled: see arm()); if that event has
+// not completed one --comm_timeout after it was recorded, or an xGMI arena's host-pinned
+// error word is set (a peer's flag missed
+// the kernel's deadline), the watchdog aborts the RCCL communicator (so its kernels
+// return) and ends the process with status 3 — the same status as a c10d collective
+// failure (utils/faults.py). A stalled peer therefore never hangs a rank forever and never
+// lets it continue on stale BN statistics.
+//
+// Ordering against the gradient buckets. The bucket all-reduces run on torch's own
+// communicator (c10d, its internal stream); the SyncBN statistics on this one, on the
+// compute stream. Each communicator's operations are issued by the main thread in the
+// same program order on every rank (the backward, and so the bucket hooks, are
+// deterministic), and each lives on a single stream, so each sees one consistent sequence
+// on all ranks. HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues in creation order,
+// identically on every rank, so wherever two streams share a queue their packets
+// interleave in the same host issue order everywhere; an RCCL kernel occupies a few CUs,
+// so two communicators' kernels are always co-resident. No rank can therefore wait on a
+// collective that its peer has queued behind a collective the first rank has not reached.
 //
 // The process links torch's own librccl.so (csrc/build.py puts torch/lib first), so there
 // is exactly one RCCL runtime in the process.
 #include "ops_decl.h"
+#include "launchers.h"
 
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace sdx_bind {
@@ -32,35 +59,175 @@ namespace sdx_bind {
 // xgmi_ops.cpp
 torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x);
 int64_t xgmi_world(int64_t id);
+int64_t xgmi_error_ext(int64_t id);
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+constexpr int kCommFailureExit = 3;   // utils/faults.py COLLECTIVE_FAILURE_EXIT_CODE
+
 enum Kind { KIND_RCCL = 1, KIND_XGMI = 2, KIND_EMU = 3 };
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
 
 struct SmallComm {
   Kind kind;
   ncclComm_t nccl = nullptr;
   int64_t xgmi_id = -1;
   int world = 1, rank = 0, device = 0;
+  double timeout_s = 600.0;
+  // watchdog state: one armed event at a time (armed by the issuing thread, cleared by
+  // the watchdog once complete)
+  hipEvent_t ev = nullptr;
+  std::atomic<bool> armed{false};
+  std::atomic<int64_t> armed_at{0};   // steady-clock ns of the armed record
+  std::atomic<long> ops{0};
 };
 
-std::mutex g_mu;
-std::vector<std::unique_ptr<SmallComm>> g_comms;   // handle = index + 1 (0 = none)
+// handle = index + 1 (0 = none). Heap-allocated and never destroyed: the detached
+// watchdog thread may still sweep it while static destructors run at process exit.
+struct Registry {
+  std::mutex mu;
+  std::vector<std::shared_ptr<SmallComm>> comms;
+};
+Registry& reg() {
+  static Registry* r = new Registry;
+  return *r;
+}
 
 void check_nccl(ncclResult_t r, const char* what) {
   TORCH_CHECK(r == ncclSuccess, what, " failed: ", ncclGetErrorString(r));
 }
 
-SmallComm& get(int64_t h) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  TORCH_CHECK(h >= 1 && h <= (int64_t)g_comms.size() && g_comms[h - 1], "bad small-communicator handle ", h);
-  return *g_comms[h - 1];
+std::shared_ptr<SmallComm> get(int64_t h) {
+  Registry& R = reg();
+  std::lock_guard<std::mutex> lk(R.mu);
+  TORCH_CHECK(h >= 1 && h <= (int64_t)R.comms.size() && R.comms[h - 1], "bad small-communicator handle ", h);
+  return R.comms[h - 1];
 }
 
-int64_t add(std::unique_ptr<SmallComm> c) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_comms.push_back(std::move(c));
-  return (int64_t)g_comms.size();
+// ---- watchdog ----------------------------------------------------------------------
+[[noreturn]] void fail_exit(SmallComm& c, const char* why) {
+  std::fprintf(stderr,
+               "rank %d: collective failure on the native SyncBN communicator (%s): %s; "
+               "aborting the process with status %d\n",
+               c.rank, c.kind == KIND_RCCL ? "RCCL" : c.kind == KIND_XGMI ? "xGMI" : "emulated", why,
+               kCommFailureExit);
+  std::fflush(stderr);
+  if (c.kind == KIND_RCCL && c.nccl) (void)ncclCommAbort(c.nccl);   // lets its kernels return
+  std::_Exit(kCommFailureExit);
+}
+
+std::atomic<bool> g_stop{false};
+std::thread* g_thread = nullptr;   // leaked on purpose (joined by the atexit hook)
+
+void watchdog_loop() {
+  while (!g_stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (g_stop.load()) break;
+    // the whole sweep holds the registry lock, so small_comm_destroy never tears down a
+    // communicator under it
+    Registry& R = reg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    for (auto& c : R.comms) {
+      if (!c || c->world <= 1) continue;
+      if (c->kind == KIND_XGMI && xgmi_error_ext(c->xgmi_id) != 0) {
+        char buf[200];
+        std::snprintf(buf, sizeof(buf), "flag of peer rank %d missed the %.0f s deadline (arena %lld)",
+                      (int)xgmi_error_ext(c->xgmi_id) - 1, c->timeout_s, (long long)c->xgmi_id);
+        fail_exit(*c, buf);
+      }
+      if (c->kind == KIND_RCCL && c->nccl) {
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+          fail_exit(*c, ncclGetErrorString(ae));
+      }
+      if (!c->armed.load(std::memory_order_acquire)) continue;
+      const hipError_t q = hipEventQuery(c->ev);
+      if (q == hipSuccess) {
+        continue;
+      } else if (q == hipErrorNotReady) {
+        const double waited = 1e-9 * (double)(now_ns() - c->armed_at.load());
+        if (waited > c->timeout_s) {
+          char buf[160];
+          std::snprintf(buf, sizeof(buf), "a collective did not complete within %.1f s (a peer died or stalled)",
+                        c->timeout_s);
+          fail_exit(*c, buf);
+        }
+      } else {
+        fail_exit(*c, hipGetErrorString(q));
+      }
+    }
+  }
+}
+
+// Stop the sweep before process teardown: the HIP runtime frees host-pinned memory (the
+// xGMI error words) and its events in its own exit hooks, which were registered before
+// this one and so run after it.
+void stop_watchdog() {
+  g_stop.store(true);
+  if (g_thread && g_thread->joinable()) g_thread->join();
+}
+
+void ensure_watchdog() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    g_thread = new std::thread(watchdog_loop);
+    std::atexit(stop_watchdog);
+  });
+}
+
+// after a collective was enqueued on `s`: move the communicator's watch event behind it
+// (re-recording a pending event is legal) and stamp the issue time, at most once per
+// 200 µs (≈30 records per ResNet-50 step instead of 106). A collective that never
+// completes keeps every later record pending, so the last record before the host blocks
+// times out. A hang inside the last < 200 µs of collectives before the host blocks is
+// caught by the next collective issued, or else by the c10d watchdog: torch's own
+// collectives (gradient buckets, loss gather, metrics) queue behind it and time out.
+// The stamp is stored BEFORE the record, so the watchdog never pairs a fresh pending
+// record with an old stamp.
+void arm(SmallComm& c, hipStream_t s) {
+  c.ops.fetch_add(1, std::memory_order_relaxed);
+  if (c.world <= 1) return;
+  const int64_t t = now_ns();
+  if (c.armed.load(std::memory_order_acquire) && t - c.armed_at.load() < 200000) return;
+  c.armed_at.store(t);
+  check_hip(hipEventRecord(c.ev, s), "hipEventRecord(watchdog)");
+  c.armed.store(true, std::memory_order_release);
+}
+
+int64_t add(std::shared_ptr<SmallComm> c) {
+  check_hip(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming), "hipEventCreate(watchdog)");
+  if (c->world > 1) ensure_watchdog();
+  Registry& R = reg();
+  std::lock_guard<std::mutex> lk(R.mu);
+  R.comms.push_back(std::move(c));
+  return (int64_t)R.comms.size();
+}
+
+// poll a non-blocking communicator until its pending operation settles (deadline)
+void settle(SmallComm& c, ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return;
+  TORCH_CHECK(r == ncclInProgress, what, " failed: ", ncclGetErrorString(r));
+  const auto t0 = Clock::now();
+  while (true) {
+    ncclResult_t ae = ncclInProgress;
+    check_nccl(ncclCommGetAsyncError(c.nccl, &ae), "ncclCommGetAsyncError");
+    if (ae == ncclSuccess) return;
+    if (ae != ncclInProgress) {
+      (void)ncclCommAbort(c.nccl);
+      c.nccl = nullptr;
+      TORCH_CHECK(false, what, " failed: ", ncclGetErrorString(ae));
+    }
+    if (std::chrono::duration<double>(Clock::now() - t0).count() > c.timeout_s) {
+      (void)ncclCommAbort(c.nccl);
+      c.nccl = nullptr;
+      TORCH_CHECK(false, what, " timed out after ", c.timeout_s, " s (a peer rank did not join or stalled)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
 }
 
 torch::Tensor rccl_unique_id() {
@@ -71,70 +238,113 @@ torch::Tensor rccl_unique_id() {
   return t;
 }
 
-int64_t rccl_comm_init(torch::Tensor id_bytes, int64_t world, int64_t rank) {
+int64_t rccl_comm_init(torch::Tensor id_bytes, int64_t world, int64_t rank, double timeout_s) {
   TORCH_CHECK(!id_bytes.is_cuda() && id_bytes.scalar_type() == at::kByte &&
                   id_bytes.numel() == (int64_t)sizeof(ncclUniqueId),
               "id: CPU uint8 [", sizeof(ncclUniqueId), "]");
   TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rank/world");
+  TORCH_CHECK(timeout_s > 0, "timeout_s > 0");
   ncclUniqueId id;
   auto ic = id_bytes.contiguous();
   std::memcpy(&id, ic.data_ptr<uint8_t>(), sizeof(id));
-  auto c = std::make_unique<SmallComm>();
+  auto c = std::make_shared<SmallComm>();
   c->kind = KIND_RCCL;
   c->world = (int)world;
   c->rank = (int)rank;
+  c->timeout_s = timeout_s;
   check_hip(hipGetDevice(&c->device), "hipGetDevice");
-  check_nccl(ncclCommInitRank(&c->nccl, (int)world, id, (int)rank), "ncclCommInitRank");
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const ncclResult_t r = ncclCommInitRankConfig(&c->nccl, (int)world, id, (int)rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (c->nccl) (void)ncclCommAbort(c->nccl);
+    TORCH_CHECK(false, "ncclCommInitRankConfig failed: ", ncclGetErrorString(r));
+  }
+  settle(*c, r, "ncclCommInitRankConfig");
   return add(std::move(c));
 }
 
-int64_t xgmi_small_comm(int64_t xgmi_id, int64_t rank) {
-  auto c = std::make_unique<SmallComm>();
+int64_t xgmi_small_comm(int64_t xgmi_id, int64_t rank, double timeout_s) {
+  auto c = std::make_shared<SmallComm>();
   c->kind = KIND_XGMI;
   c->xgmi_id = xgmi_id;
   c->world = (int)xgmi_world(xgmi_id);
   c->rank = (int)rank;
+  c->timeout_s = timeout_s;
   check_hip(hipGetDevice(&c->device), "hipGetDevice");
   return add(std::move(c));
 }
 
-int64_t emu_small_comm(int64_t world) {
+int64_t emu_small_comm(int64_t world, double timeout_s) {
   TORCH_CHECK(world >= 1, "world >= 1");
-  auto c = std::make_unique<SmallComm>();
+  auto c = std::make_shared<SmallComm>();
   c->kind = KIND_EMU;
   c->world = (int)world;
+  c->timeout_s = timeout_s;
   check_hip(hipGetDevice(&c->device), "hipGetDevice");
   return add(std::move(c));
 }
 
 void small_comm_destroy(int64_t h) {
-  std::unique_ptr<SmallComm> c;
+  std::shared_ptr<SmallComm> c;
   {
-    std::lock_guard<std::mutex> lk(g_mu);
-    TORCH_CHECK(h >= 1 && h <= (int64_t)g_comms.size() && g_comms[h - 1], "bad small-communicator handle ", h);
-    c = std::move(g_comms[h - 1]);
+    Registry& R = reg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    TORCH_CHECK(h >= 1 && h <= (int64_t)R.comms.size() && R.comms[h - 1], "bad small-communicator handle ", h);
+    c = std::move(R.comms[h - 1]);   // out of the watchdog's sight from here on
   }
   if (c->kind == KIND_RCCL && c->nccl) {
     (void)hipDeviceSynchronize();
     (void)ncclCommDestroy(c->nccl);
+    c->nccl = nullptr;
   }
+  if (c->ev) (void)hipEventDestroy(c->ev);
+}
+
+// local teardown for a failed set-up (ranks agreed to fall back): ncclCommAbort never
+// waits for peers, unlike a destroy that may flush operations they will never match
+void small_comm_abort(int64_t h) {
+  std::shared_ptr<SmallComm> c;
+  {
+    Registry& R = reg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    TORCH_CHECK(h >= 1 && h <= (int64_t)R.comms.size() && R.comms[h - 1], "bad small-communicator handle ", h);
+    c = std::move(R.comms[h - 1]);
+  }
+  if (c->kind == KIND_RCCL && c->nccl) {
+    (void)ncclCommAbort(c->nccl);
+    c->nccl = nullptr;
+  }
+  if (c->ev) (void)hipEventDestroy(c->ev);
 }
 
 void small_all_reduce_py(int64_t h, torch::Tensor x) { small_all_reduce_(h, x); }
 
+// watchdog drill: a bounded GPU stall (seconds) on the current stream followed by a
+// collective on handle h, so the armed event waits behind the stall
+void small_comm_stall_(int64_t h, double seconds, torch::Tensor x) {
+  check_hip(launch_gpu_stall((long long)(seconds * 1e8), cur_stream()), "gpu_stall");
+  small_all_reduce_(h, x);
+}
+
+int64_t small_comm_ops(int64_t h) { return get(h)->ops.load(); }
+
 }  // namespace
 
-int small_comm_world(int64_t h) { return h == 0 ? 1 : get(h).world; }
+int small_comm_world(int64_t h) { return h == 0 ? 1 : get(h)->world; }
 
 // in-place SUM over the communicator's ranks, ordered on the current stream
 void small_all_reduce_(int64_t h, torch::Tensor& x) {
   if (h == 0) return;
-  SmallComm& c = get(h);
+  auto cp = get(h);
+  SmallComm& c = *cp;
   TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "small all-reduce: contiguous GPU tensor");
   TORCH_CHECK(x.device().index() == c.device, "small all-reduce: tensor on device ", x.device().index(),
               ", communicator on ", c.device);
   if (c.world == 1) return;
+  hipStream_t s = cur_stream();
   if (c.kind == KIND_RCCL) {
+    TORCH_CHECK(c.nccl, "small all-reduce: RCCL communicator was aborted");
     ncclDataType_t dt;
     switch (x.scalar_type()) {
       case at::kDouble: dt = ncclFloat64; break;
@@ -142,8 +352,7 @@ void small_all_reduce_(int64_t h, torch::Tensor& x) {
       case at::kInt: dt = ncclInt32; break;
       default: TORCH_CHECK(false, "small all-reduce: fp64 / fp32 / int32 only");
     }
-    check_nccl(ncclAllReduce(x.data_ptr(), x.data_ptr(), (size_t)x.numel(), dt, ncclSum, c.nccl, cur_stream()),
-               "ncclAllReduce");
+    settle(c, ncclAllReduce(x.data_ptr(), x.data_ptr(), (size_t)x.numel(), dt, ncclSum, c.nccl, s), "ncclAllReduce");
   } else if (c.kind == KIND_EMU) {
     x.mul_((double)c.world);
   } else {
@@ -151,17 +360,25 @@ void small_all_reduce_(int64_t h, torch::Tensor& x) {
     auto r = xgmi_allreduce_ext(c.xgmi_id, x);
     x.copy_(r);
   }
+  arm(c, s);
 }
 
 void register_comm(pybind11::module& m) {
   m.def("rccl_unique_id", &rccl_unique_id, "ncclGetUniqueId as CPU uint8 bytes (rank 0; broadcast it)");
-  m.def("rccl_comm_init", &rccl_comm_init, "dedicated RCCL communicator for SyncBN statistics -> handle",
-        pybind11::arg("id"), pybind11::arg("world"), pybind11::arg("rank"));
-  m.def("xgmi_small_comm", &xgmi_small_comm, "wrap a one-shot xGMI arena as a small-communicator handle");
-  m.def("emu_small_comm", &emu_small_comm, "W identical virtual ranks in one process (tests): sum = x*W");
+  m.def("rccl_comm_init", &rccl_comm_init,
+        "dedicated non-blocking RCCL communicator for SyncBN statistics (init polled against timeout_s) -> handle",
+        pybind11::arg("id"), pybind11::arg("world"), pybind11::arg("rank"), pybind11::arg("timeout_s") = 600.0);
+  m.def("xgmi_small_comm", &xgmi_small_comm, "wrap a one-shot xGMI arena as a small-communicator handle",
+        pybind11::arg("xgmi_id"), pybind11::arg("rank"), pybind11::arg("timeout_s") = 600.0);
+  m.def("emu_small_comm", &emu_small_comm, "W identical virtual ranks in one process (tests): sum = x*W",
+        pybind11::arg("world"), pybind11::arg("timeout_s") = 600.0);
   m.def("small_comm_destroy", &small_comm_destroy);
+  m.def("small_comm_abort", &small_comm_abort, "local abort of a communicator whose set-up the ranks gave up");
   m.def("small_comm_world", &small_comm_world);
+  m.def("small_comm_ops", &small_comm_ops, "collectives issued on a handle so far");
   m.def("small_all_reduce_", &small_all_reduce_py, "in-place SUM on the current stream");
+  m.def("small_comm_stall_", &small_comm_stall_,
+        "watchdog drill: bounded GPU stall, then a collective whose completion event waits behind it");
 }
 
 }  // namespace sdx_bind

@@ -530,7 +530,7 @@ struct CoefOut {
 BnCoefArgs coef_args(const torch::Tensor& like, int64_t C, int nsets, double count, const OptT& g_a,
                      const torch::Tensor& mean_a, const torch::Tensor& inv_a, const OptT& g_b, const OptT& mean_b,
                      const OptT& inv_b, const OptT& sink_ga, const OptT& sink_ba, const OptT& sink_gb,
-                     const OptT& sink_bb, CoefOut& o) {
+                     const OptT& sink_bb, CoefOut& o, double grad_scale = 1.0) {
   TORCH_CHECK(nsets == 1 || nsets == 2, "1 or 2 BN sets");
   check_vec(mean_a, C, "mean_a");
   check_vec(inv_a, C, "inv_a");
@@ -541,6 +541,7 @@ BnCoefArgs coef_args(const torch::Tensor& like, int64_t C, int nsets, double cou
   BnCoefArgs a{};
   a.count = count;
   a.accumulate = sinks ? 1 : 0;
+  a.grad_scale = grad_scale;
   o.coef_a = torch::empty({3, C}, fo);
   o.dga = sinks ? *sink_ga : torch::empty({C}, fo);
   o.dba = sinks ? *sink_ba : torch::empty({C}, fo);
@@ -577,7 +578,7 @@ BnCoefArgs coef_args(const torch::Tensor& like, int64_t C, int nsets, double cou
 
 std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_a, torch::Tensor mean_a,
                                        torch::Tensor inv_a, OptT g_b, OptT mean_b, OptT inv_b, OptT sink_ga,
-                                       OptT sink_ba, OptT sink_gb, OptT sink_bb) {
+                                       OptT sink_ba, OptT sink_gb, OptT sink_bb, double grad_scale = 1.0) {
   TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.dim() == 2 && sums.is_contiguous(),
               "sums must be [nsets+1, C] float64");
   const int64_t C = sums.size(1);
@@ -585,7 +586,7 @@ std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_
   c10::DeviceGuard dg(sums.device());
   CoefOut o;
   const BnCoefArgs a = coef_args(sums, C, nsets, count, g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga, sink_ba,
-                                 sink_gb, sink_bb, o);
+                                 sink_gb, sink_bb, o, grad_scale);
   check_hip(launch_bn_bwd_coef(sums.data_ptr<double>(), nsets, C, a, cur_stream()), "bn_bwd_coef");
   return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
 }
@@ -708,8 +709,8 @@ std::vector<torch::Tensor> bn_bwd_sync(int64_t comm, torch::Tensor dout, OptT ou
                               sink_gb, sink_bb);
   auto sums = bn_bwd_reduce(dout, outv, ya, ma, yb, mb, msc, msh);
   small_all_reduce_(comm, sums);
-  return bn_bwd_coef(sums, count * small_comm_world(comm), g_a, ma, inv_a, g_b, mb, inv_b, sink_ga, sink_ba, sink_gb,
-                     sink_bb);
+  const int w = small_comm_world(comm);
+  return bn_bwd_coef(sums, count * w, g_a, ma, inv_a, g_b, mb, inv_b, sink_ga, sink_ba, sink_gb, sink_bb, 1.0 / w);
 }
 
 // event pool for side-stream fork points
@@ -745,8 +746,9 @@ std::vector<torch::Tensor> bn_bwd_coef_slab(int64_t comm, torch::Tensor slab, do
                                 cur_stream()),
               "bn_bwd_coef_slab(reduce)");
     small_all_reduce_(comm, sums);
-    return bn_bwd_coef(sums, count * small_comm_world(comm), g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga, sink_ba,
-                       sink_gb, sink_bb);
+    const int w = small_comm_world(comm);
+    return bn_bwd_coef(sums, count * w, g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga, sink_ba, sink_gb, sink_bb,
+                       1.0 / w);
   }
   CoefOut o;
   const BnCoefArgs a = coef_args(slab, C, (int)nsum - 1, count, g_a, mean_a, inv_a, g_b, mean_b, inv_b, sink_ga,
@@ -1020,7 +1022,8 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),
         pybind11::arg("mean_b") = pybind11::none(), pybind11::arg("inv_b") = pybind11::none(),
         pybind11::arg("sink_ga") = pybind11::none(), pybind11::arg("sink_ba") = pybind11::none(),
-        pybind11::arg("sink_gb") = pybind11::none(), pybind11::arg("sink_bb") = pybind11::none());
+        pybind11::arg("sink_gb") = pybind11::none(), pybind11::arg("sink_bb") = pybind11::none(),
+        pybind11::arg("grad_scale") = 1.0);
   m.def("bn_bwd_reduce_coef", &bn_bwd_reduce_coef, pybind11::arg("dout"), pybind11::arg("outv"),
         pybind11::arg("ya"), pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(),
         pybind11::arg("mb") = pybind11::none(), pybind11::arg("msc") = pybind11::none(),

@@ -20,7 +20,8 @@ struct Arena {
   std::vector<void*> opened;       // peer arenas mapped through IPC
   XgmiPeers peers{};
   unsigned epoch = 0;
-  torch::Tensor err;               // device int32 error word (sender index + 1)
+  int* err = nullptr;              // host-pinned, GPU-written error word (sender index + 1)
+  long long timeout_ticks = 0;     // flag-poll deadline in 100 MHz wall-clock ticks
 };
 
 std::mutex g_mu;
@@ -42,9 +43,10 @@ void set_ptrs(XgmiPeers& p, int q, void* base, int world, size_t cap) {
   p.flags[q] = reinterpret_cast<unsigned*>(static_cast<char*>(base) + 2ull * world * cap * sizeof(double));
 }
 
-int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap) {
+int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, double timeout_s) {
   TORCH_CHECK(world >= 1 && world <= kXgmiMaxPeers && rank >= 0 && rank < world, "1 <= world <= 8");
   TORCH_CHECK(cap > 0 && cap <= (1 << 20), "cap in (0, 2^20]");
+  TORCH_CHECK(timeout_s > 0 && timeout_s < 86400, "timeout_s in (0, 1 day)");
   auto a = std::make_unique<Arena>();
   check_hip(hipGetDevice(&a->device), "hipGetDevice");
   a->rank = (int)rank;
@@ -56,7 +58,14 @@ int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap) {
   check_hip(hipMemset(a->base, 0, bytes), "hipMemset");
   a->peers.cap = a->cap;
   set_ptrs(a->peers, a->rank, a->base, a->world, a->cap);
-  a->err = torch::zeros({1}, torch::TensorOptions().dtype(at::kInt).device(torch::kCUDA, a->device));
+  // error word in coherent host memory: the kernel stores it (system scope) and the host
+  // watchdog (comm_ops.cpp) polls it with plain loads — no device copy on any stream
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&a->err), sizeof(int), hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(err)");
+  *reinterpret_cast<volatile int*>(a->err) = 0;
+  int rate_khz = 0;
+  check_hip(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, a->device), "wall clock rate");
+  a->timeout_ticks = (long long)(timeout_s * 1000.0 * (rate_khz > 0 ? rate_khz : 100000));
   std::lock_guard<std::mutex> lk(g_mu);
   g_arenas.push_back(std::move(a));
   return (int64_t)g_arenas.size() - 1;
@@ -96,14 +105,14 @@ torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x) {
   auto out = torch::empty_like(x);
   a.epoch += 1;
   check_hip(launch_xgmi_allreduce(x.data_ptr<double>(), out.data_ptr<double>(), (int)x.numel(), a.peers, a.rank,
-                                  a.world, a.epoch, a.err.data_ptr<int>(), cur_stream()),
+                                  a.world, a.epoch, a.err, a.timeout_ticks, cur_stream()),
             "xgmi_allreduce");
   return out;
 }
 
 int64_t xgmi_error(int64_t id) {
   Arena& a = get(id);
-  return a.err.cpu().item<int>();
+  return *reinterpret_cast<volatile int*>(a.err);
 }
 
 void xgmi_destroy(int64_t id) {
@@ -116,6 +125,7 @@ void xgmi_destroy(int64_t id) {
   (void)hipDeviceSynchronize();
   for (void* p : a->opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(a->base);
+  (void)hipHostFree(a->err);
 }
 
 // W virtual ranks on this GPU: `in` [W, n] fp64; runs `iters` calls (epochs 1..iters, so both
@@ -152,14 +162,21 @@ torch::Tensor xgmi_emulate(torch::Tensor in, int64_t iters) {
 // for comm_ops.cpp (small-communicator wrapper of an arena)
 torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x) { return xgmi_allreduce(id, x); }
 int64_t xgmi_world(int64_t id) { return get(id).world; }
+int64_t xgmi_error_ext(int64_t id) { return xgmi_error(id); }
+std::vector<int64_t> xgmi_debug(int64_t id) {
+  Arena& a = get(id);
+  return {(int64_t)(uintptr_t)a.err, (int64_t)*reinterpret_cast<volatile int*>(a.err), (int64_t)a.world};
+}
 
 void register_xgmi(pybind11::module& m) {
-  m.def("xgmi_create", &xgmi_create, "allocate this rank's IPC receive arena (uncached device memory)");
+  m.def("xgmi_create", &xgmi_create, "allocate this rank's IPC receive arena (uncached device memory)",
+        pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("cap"), pybind11::arg("timeout_s") = 600.0);
   m.def("xgmi_handle", &xgmi_handle, "64-byte IPC handle of this rank's arena");
   m.def("xgmi_open", &xgmi_open, "map every peer's arena from their IPC handles [W, 64]");
   m.def("xgmi_allreduce", &xgmi_allreduce, "one-shot fp64 all-reduce (sum) of a small tensor");
   m.def("xgmi_error", &xgmi_error, "nonzero: a peer's flag never arrived (1 + sender)");
   m.def("xgmi_destroy", &xgmi_destroy);
+  m.def("xgmi_debug", &xgmi_debug);
   m.def("xgmi_emulate", &xgmi_emulate, "single-GPU W-rank emulation of the one-shot protocol");
 }
 

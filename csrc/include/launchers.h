@@ -88,6 +88,11 @@ struct BnCoefArgs {
   const float *g_a, *mean_a, *inv_a, *g_b, *mean_b, *inv_b;
   float *coef_a, *coef_b, *dgamma_a, *dbeta_a, *dgamma_b, *dbeta_b;
   int accumulate;
+  // factor on the dγ/dβ written to the sinks. SyncBN over W ranks sums Σdz, Σdz·ŷ over the
+  // ranks before the coefficients; the parameter gradient must stay this rank's share
+  // (global / W, like torch SyncBatchNorm's local grad_weight after the DDP mean), so the
+  // bucket reducer's sum × 1/W yields global / W and not the global value.
+  double grad_scale = 1.0;
 };
 // Deterministic reduction of a [rows][nsets][C] fp32 slab to fp64 sums [nsets][C] in ONE
 // launch (per-block partials + last-arriver combine; no memset). epi: 0 sums only,
@@ -146,7 +151,11 @@ struct XgmiPeers {
   unsigned* flags[kXgmiMaxPeers];  // each rank's flags: [2][W] u32
   size_t cap;                      // elements per slot
 };
+// err: host-pinned int (1 + rank of a peer whose flag missed the deadline of timeout_ticks
+// of the 100 MHz wall clock; the sum is then skipped)
 hipError_t launch_xgmi_allreduce(const double* in, double* out, int n, const XgmiPeers& peers, int me, int world,
-                                 unsigned epoch, int* err, hipStream_t s);
+                                 unsigned epoch, int* err, long long timeout_ticks, hipStream_t s);
+// bounded single-wave sleep on stream s (watchdog tests)
+hipError_t launch_gpu_stall(long long ticks, hipStream_t s);
 hipError_t launch_xgmi_emulate(const double* in, double* out, int n, const XgmiPeers& peers, int world,
                                unsigned epoch, int* err, hipStream_t s);

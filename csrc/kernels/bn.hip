@@ -61,8 +61,8 @@ __device__ __forceinline__ void bn_coef_one(int c, int C, const double* s, int n
     coef[2 * C + c] = (float)E;
     float* dg = set == 0 ? a.dgamma_a : a.dgamma_b;
     float* db = set == 0 ? a.dbeta_a : a.dbeta_b;
-    if (dg) dg[c] = (float)(sdzy * inv) + (a.accumulate ? dg[c] : 0.f);
-    if (db) db[c] = (float)sdz + (a.accumulate ? db[c] : 0.f);
+    if (dg) dg[c] = (float)(sdzy * inv * a.grad_scale) + (a.accumulate ? dg[c] : 0.f);
+    if (db) db[c] = (float)(sdz * a.grad_scale) + (a.accumulate ? db[c] : 0.f);
   }
 }
 

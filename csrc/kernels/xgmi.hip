@@ -9,9 +9,13 @@
 //      (remote stores travel over the point-to-point xGMI link to that peer);
 //   2. each storing wave drains its stores, then one lane publishes `e` into flags
 //      [parity][me] of every arena with a system-scope release store;
-//   3. each rank polls its own W flags (bounded spin: a dead or lagging peer reports an
-//      error instead of hanging the GPU), acquires, and sums the W slots in rank order —
-//      every rank computes bit-identical results.
+//   3. each rank polls its own W flags, acquires, and sums the W slots in rank order —
+//      every rank computes bit-identical results. The poll is bounded by a wall-clock
+//      deadline (the 100 MHz constant clock, --comm_timeout): a dead or lagging peer makes
+//      the kernel give up, skip the sum and store 1 + that peer's rank into the error word,
+//      which lives in host-pinned memory — the native communicator's host watchdog
+//      (comm_ops.cpp) reads it without a device copy and ends the process with status 3
+//      instead of training on stale statistics.
 // Two parities make the arena reusable without a second barrier: a rank can only start
 // call e+2 (same parity) after it saw every peer's flag for e+1, which each peer wrote
 // after it had finished reading call e.
@@ -26,11 +30,10 @@ using namespace sdx;
 
 namespace {
 
-constexpr unsigned kSpinLimit = 1u << 26;   // ~ tens of ms of polling before giving up
 
 template <int SCOPE>
 __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__ out, int n, const XgmiPeers& peers,
-                             int me, int world, unsigned epoch, int* err) {
+                             int me, int world, unsigned epoch, int* err, long long timeout_ticks) {
   const int par = epoch & 1;
   const size_t cap = peers.cap;
   // 1. scatter my contribution into every arena
@@ -56,14 +59,16 @@ __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__
   __syncthreads();
   if (threadIdx.x < world) {
     unsigned* f = peers.flags[me] + par * world + threadIdx.x;
+    const long long t0 = wall_clock64();
     unsigned spins = 0;
     while (true) {
       const unsigned v = SCOPE == 1 ? __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
                                     : __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       if (v == epoch) break;
-      if (++spins > kSpinLimit) {
+      if ((++spins & 63) == 0 && wall_clock64() - t0 > timeout_ticks) {
         atomicExch(&ok_all, 0);
-        if (err) atomicExch(err, 1 + (int)threadIdx.x);
+        // host-pinned word for the real arena (system scope), device word for the emulation
+        if (err) __hip_atomic_store(err, 1 + (int)threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -86,23 +91,34 @@ __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__
 }
 
 __global__ __launch_bounds__(256) void oneshot_kernel(const double* in, double* out, int n, XgmiPeers peers, int me,
-                                                      int world, unsigned epoch, int* err) {
-  oneshot_body<1>(in, out, n, peers, me, world, epoch, err);
+                                                      int world, unsigned epoch, int* err, long long timeout_ticks) {
+  oneshot_body<1>(in, out, n, peers, me, world, epoch, err, timeout_ticks);
 }
 
 // block b = virtual rank b; in/out are [W][n]; peers.data/flags are the W local arenas
 __global__ __launch_bounds__(256) void oneshot_emulate_kernel(const double* in, double* out, int n, XgmiPeers peers,
                                                               int world, unsigned epoch, int* err) {
   const int me = blockIdx.x;
-  oneshot_body<0>(in + (size_t)me * n, out + (size_t)me * n, n, peers, me, world, epoch, err);
+  // all virtual ranks are co-resident blocks of this launch: a missing flag is a protocol
+  // bug, reported after ~1 s of the 100 MHz clock
+  oneshot_body<0>(in + (size_t)me * n, out + (size_t)me * n, n, peers, me, world, epoch, err, 100000000LL);
+}
+
+// Bounded GPU stall for the watchdog tests: one wave sleeps until `ticks` of the 100 MHz
+// constant clock have passed (never longer), standing in for a collective whose peer hangs.
+__global__ __launch_bounds__(64) void stall_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 }  // namespace
 
 hipError_t launch_xgmi_allreduce(const double* in, double* out, int n, const XgmiPeers& peers, int me, int world,
-                                 unsigned epoch, int* err, hipStream_t s) {
-  if (n < 0 || (size_t)n > peers.cap || world < 1 || world > kXgmiMaxPeers) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(oneshot_kernel, dim3(1), dim3(256), 0, s, in, out, n, peers, me, world, epoch, err);
+                                 unsigned epoch, int* err, long long timeout_ticks, hipStream_t s) {
+  if (n < 0 || (size_t)n > peers.cap || world < 1 || world > kXgmiMaxPeers || timeout_ticks <= 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(oneshot_kernel, dim3(1), dim3(256), 0, s, in, out, n, peers, me, world, epoch, err,
+                     timeout_ticks);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -111,6 +127,13 @@ hipError_t launch_xgmi_emulate(const double* in, double* out, int n, const XgmiP
                                unsigned epoch, int* err, hipStream_t s) {
   if (n < 0 || (size_t)n > peers.cap || world < 1 || world > kXgmiMaxPeers) return hipErrorInvalidValue;
   hipLaunchKernelGGL(oneshot_emulate_kernel, dim3(world), dim3(256), 0, s, in, out, n, peers, world, epoch, err);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_gpu_stall(long long ticks, hipStream_t s) {
+  if (ticks < 0 || ticks > 2000000000LL) return hipErrorInvalidValue;   // at most 20 s
+  hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, ticks);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -66,7 +66,8 @@ class LinearEngine:
         va = build_dataset(opt.dataset, opt.data_folder, False, opt.synthetic, opt.synthetic_size, 32, opt.seed)
         self.tr_x, self.tr_y = torch.from_numpy(tr.images).to(dev), torch.from_numpy(tr.labels).to(dev)
         self.va_x, self.va_y = torch.from_numpy(va.images).to(dev), torch.from_numpy(va.labels).to(dev)
-        self.sampler = DistributedIndexSampler(len(tr), opt.batch_size, 1, 0, seed=opt.seed)
+        # the reference DataLoader keeps the last partial batch (main_ce.py set_loader)
+        self.sampler = DistributedIndexSampler(len(tr), opt.batch_size, 1, 0, seed=opt.seed, drop_last=False)
         self.aug_train = AugConfig.linear_train(32, opt.mean_t, opt.std_t)
         self.aug_val = AugConfig.evaluation(32, opt.mean_t, opt.std_t)
         from ..utils.tb import Logger
@@ -87,6 +88,9 @@ class LinearEngine:
         if opt.max_steps:
             iters = min(iters, opt.max_steps)
         bt, dtm, losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter(), AverageMeter(), AverageMeter()
+        # every batch counts in the epoch meters (reference main_linear.py:151-155): the sums
+        # stay on the device and reach the host once per print window
+        win = torch.zeros(4, dtype=torch.float64, device=self.device)   # Σloss·b, Σacc1·b, Σacc5·b, Σb
         end = time.time()
         for idx_i, idx in enumerate(self.sampler.batches(self.device)):
             if idx_i >= iters:
@@ -107,11 +111,17 @@ class LinearEngine:
                 self.optimizer.zero_grad()
                 loss.backward()
                 self.optimizer.step()
+                win += torch.stack([loss.detach().double() * bsz, acc1[0].double() * bsz, acc5[0].double() * bsz,
+                                    torch.tensor(float(bsz), dtype=torch.float64, device=self.device)])
+            bt.update(time.time() - end)
             if (idx_i + 1) % opt.print_freq == 0 or idx_i + 1 == iters:
-                losses.update(loss.item(), bsz)
-                top1.update(acc1[0].item(), bsz)
-                top5.update(acc5[0].item(), bsz)
-                bt.update(time.time() - end)
+                sl, s1, s5, nb = win.tolist()       # one host sync per print window
+                win.zero_()
+                losses.update(sl / nb, nb)
+                losses.val = loss.item()
+                top1.update(s1 / nb, nb)
+                top1.val = acc1[0].item()
+                top5.update(s5 / nb, nb)
                 logging.info("Train: [{0}][{1}/{2}]\tBT {bt.val:.3f} ({bt.avg:.3f})\t"
                              "DT {dt.val:.3f} ({dt.avg:.3f})\tloss {loss.val:.3f} ({loss.avg:.3f})\t"
                              "Acc@1 {top1.val:.3f} ({top1.avg:.3f})".format(

@@ -148,31 +148,27 @@ class PretrainEngine:
         want = getattr(opt, "syncbn_comm", "rccl")
         if dev.type != "cuda":
             return
+        timeout = float(getattr(opt, "comm_timeout", 600.0))
         if want == "xgmi":
+            # set-up is agreed step by step across ranks (parallel/xgmi.py): either every
+            # rank gets the arena or every rank raises here and falls back to RCCL together
             try:
                 from ..parallel.xgmi import OneShotAllReduce
-                impl = OneShotAllReduce()
+                impl = OneShotAllReduce(timeout_s=timeout)
                 comm.set_small_allreduce(None, impl)
-                comm.set_native_small_comm(None, _ext.require().xgmi_small_comm(impl.id, comm.rank()))
+                comm.set_native_small_comm(None, _ext.require().xgmi_small_comm(impl.id, comm.rank(), timeout))
                 logging.info("SyncBN statistics: one-shot xGMI all-reduce (native executor)")
                 return
             except Exception as e:  # noqa: BLE001
                 logging.warning(f"one-shot xGMI all-reduce unavailable ({e}); using RCCL")
         if comm.backend() == "nccl" and os.environ.get("SDX_NATIVE_SYNCBN", "1") != "0":
-            handle, err = 0, None
-            try:
-                handle = comm.create_rccl_small_comm(None)
-            except Exception as e:  # noqa: BLE001
-                err = e
-            # every rank must agree, or the BN collectives would be mismatched across ranks
-            ok = torch.tensor([0.0 if err is not None else 1.0], device=dev)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if ok.item() == 1.0:
+            # 0 on every rank together when the dedicated communicator cannot be set up
+            handle = comm.create_rccl_small_comm(None, timeout)
+            if handle:
                 comm.set_native_small_comm(None, handle)
                 logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
             else:
-                logging.warning(f"dedicated RCCL communicator unavailable on some rank ({err}); "
-                                "SyncBN statistics use the process-group all-reduce")
+                logging.warning("SyncBN statistics use the process-group all-reduce")
 
     def _resume(self, path):
         st = ckpt_mod.load_checkpoint(path)
@@ -311,11 +307,19 @@ class PretrainEngine:
     def enable_cuda_graph(self, idx_example: torch.Tensor, warmup: int = 2) -> bool:
         """Capture the whole training step (aug → fwd → loss → bwd → SGD) in one hipGraph.
 
-        Single-process only (the data-parallel path keeps eager launches). Warm-up steps are
-        real training steps run on a side stream, as graph capture requires."""
+        Single-process only (the data-parallel path keeps eager launches). Capture needs
+        warm-up steps run on a side stream; they execute real updates, so the training
+        state they touch (parameters, optimizer buffers, BN running statistics, the norm
+        EMA) is snapshotted first and restored after the capture — a graphed run follows
+        exactly the eager trajectory."""
         if self.device.type != "cuda" or self.world > 1 or self.backend != "native":
             return False
         self._idx_buf = idx_example.clone()
+        state = [self.flat.flat, self.optimizer.buf, self.record_norm_mean, self._rnm_valid]
+        state += [t for t in self.model.buffers()]
+        if getattr(self.optimizer, "norms", None) is not None:
+            state.append(self.optimizer.norms)
+        snap = [t.detach().clone() for t in state]
         self._host_prelude(1, 0, 1)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
@@ -327,6 +331,9 @@ class PretrainEngine:
         with torch.cuda.graph(g):
             self._graph_stats = self._step_body(self._idx_buf)
         self._graph = g
+        with torch.no_grad():
+            for t, v in zip(state, snap):
+                t.copy_(v)
         return True
 
     def _norm_terms(self, feats):

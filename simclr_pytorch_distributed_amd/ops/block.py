@@ -102,7 +102,9 @@ def _bn_bwd(m, dout, out, y, mean, inv, bn, count, group, y_b=None, mean_b=None,
     else:
         s = m.bn_bwd_reduce(dout, out, y, mean, y_b, mean_b, msc, msh)
         comm.small_all_reduce_(s, group)
-        ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, gb, mean_b, inv_b, **snk)
+        # dγ/dβ: this rank's share of the all-reduced sums (torch SyncBatchNorm + DDP mean)
+        ca, cb, _, _, _, _ = m.bn_bwd_coef(s, float(count), bn.weight.detach(), mean, inv, gb, mean_b, inv_b, **snk,
+                                           grad_scale=1.0 / _world(group))
     if y_b is None:
         dya, _, dz = m.bn_bwd_apply(dout, out, y, ca, None, None, want_dz, msc, msh)
         return dya, None, dz

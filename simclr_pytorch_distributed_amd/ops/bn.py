@@ -31,6 +31,13 @@ def _world(group) -> int:
     return dist.get_world_size(group) if group is not None else 1
 
 
+def _gscale(group) -> float:
+    """dγ/dβ factor: the backward sums are all-reduced (global), but the parameter
+    gradient must stay this rank's share — torch SyncBatchNorm returns the local
+    grad_weight/grad_bias, which the DDP mean turns into global / W."""
+    return 1.0 / _world(group)
+
+
 def _finalize(m, sums, bn, count, training, group):
     if training:
         _allreduce(sums, group)
@@ -64,7 +71,8 @@ class _BNAct(torch.autograd.Function):
         dout = dout.contiguous()
         s = m.bn_bwd_reduce(dout, out, y, mean, None, None)
         _allreduce(s, ctx.group)
-        ca, _, dga, dba, _, _ = m.bn_bwd_coef(s, float(ctx.count), gamma.detach(), mean, inv, None, None, None)
+        ca, _, dga, dba, _, _ = m.bn_bwd_coef(s, float(ctx.count), gamma.detach(), mean, inv, None, None, None,
+                                              grad_scale=_gscale(ctx.group))
         dy, _, _ = m.bn_bwd_apply(dout, out, y, ca, None, None, False)
         return dy, None, dga, dba, None, None, None, None
 
@@ -98,12 +106,13 @@ class _BNAddAct(torch.autograd.Function):
             s = m.bn_bwd_reduce(dout, out, ya, mean_a, yb, mean_b)
             _allreduce(s, ctx.group)
             ca, cb, dga, dba, dgb, dbb = m.bn_bwd_coef(s, float(ctx.count), ga.detach(), mean_a, inv_a,
-                                                       gb.detach(), mean_b, inv_b)
+                                                       gb.detach(), mean_b, inv_b, grad_scale=_gscale(ctx.group))
             dya, dyb, _ = m.bn_bwd_apply(dout, out, ya, ca, yb, cb, False)
             return dya, None, dga, dba, dyb, None, dgb, dbb, None, None, None, None, None
         s = m.bn_bwd_reduce(dout, out, ya, mean_a, None, None)
         _allreduce(s, ctx.group)
-        ca, _, dga, dba, _, _ = m.bn_bwd_coef(s, float(ctx.count), ga.detach(), mean_a, inv_a, None, None, None)
+        ca, _, dga, dba, _, _ = m.bn_bwd_coef(s, float(ctx.count), ga.detach(), mean_a, inv_a, None, None, None,
+                                              grad_scale=_gscale(ctx.group))
         dya, _, dz = m.bn_bwd_apply(dout, out, ya, ca, None, None, True)
         return dya, None, dga, dba, None, None, None, None, dz, None, None, None, None
 

@@ -159,28 +159,94 @@ def native_small_comm(group) -> int:
     return _native.get(_key(group), 0)
 
 
-def create_rccl_small_comm(group=None) -> int:
-    """A dedicated RCCL communicator over ``group``'s ranks for SyncBN statistics.
+def _agree_device(group=None) -> torch.device:
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def agree(ok: bool, group=None) -> bool:
+    """True on every rank iff ``ok`` is true on every rank (one MIN all-reduce)."""
+    if not is_dist():
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_agree_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def negotiate(steps, cleanup, group=None):
+    """Run a multi-step set-up in which ranks must stay in lock-step.
+
+    ``steps``: callables run in order on every rank. A step that runs a collective must
+    be reached by all ranks or by none, so after EACH step the ranks agree (MIN
+    all-reduce) that it succeeded everywhere before any rank starts the next one. If a
+    step failed on any rank, every rank calls ``cleanup()`` (which must undo whatever
+    part of the set-up this rank completed) and the function returns ``(False, err)``
+    with this rank's own error (None where it succeeded) — all ranks together.
+    """
+    err = None
+    for st in steps:
+        try:
+            st()
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not agree(err is None, group):
+            try:
+                cleanup()
+            except Exception:  # noqa: BLE001
+                pass
+            return False, err
+    return True, None
+
+
+def create_rccl_small_comm(group=None, timeout_s: float = 600.0) -> int:
+    """A dedicated RCCL communicator over ``group``'s ranks for SyncBN statistics, or 0
+    (on every rank together) if it cannot be set up anywhere.
 
     Rank 0 draws an ``ncclUniqueId`` and broadcasts it through the process group
     (the TCP/env rendezvous only carries this id); every rank then joins
-    with ``ncclCommInitRank``. Kept apart from torch's communicators, so the gradient
-    buckets on the reducer's comm stream never queue in front of a BN statistic.
+    with a non-blocking ``ncclCommInitRankConfig`` polled against ``timeout_s`` and runs a
+    self-check all-reduce. The ranks agree after every step (:func:`negotiate`), so a
+    failure on one rank never leaves the others inside a mismatched collective; handles
+    created before a failure are aborted locally. Kept apart from torch's communicators,
+    so the gradient buckets on the reducer's comm stream never queue in front of a BN
+    statistic (ordering argument: csrc/bindings/comm_ops.cpp).
     """
     from ..ops import _ext
     m = _ext.require()
     w, r = dist.get_world_size(group), dist.get_rank(group)
     dev = torch.device("cuda", torch.cuda.current_device())
-    uid = m.rccl_unique_id() if r == 0 else torch.zeros(128, dtype=torch.uint8)
-    t = uid.to(dev) if backend() == "nccl" else uid
-    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-    h = m.rccl_comm_init(t.cpu(), w, r)
-    # one warm-up all-reduce: fails loudly here rather than inside the first forward
-    probe = torch.ones(4, dtype=torch.float64, device=dev)
-    m.small_all_reduce_(h, probe)
-    if float(probe[0].item()) != float(w):
-        raise RuntimeError(f"RCCL small communicator self-check failed ({probe[0].item()} != {w})")
-    return h
+    st = {"uid": torch.zeros(128, dtype=torch.uint8), "h": 0}
+
+    def draw():
+        if r == 0:
+            st["uid"] = m.rccl_unique_id()
+
+    def share():
+        t = st["uid"].to(dev) if backend() == "nccl" else st["uid"]
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        st["uid"] = t.cpu()
+
+    def join():
+        st["h"] = m.rccl_comm_init(st["uid"], w, r, float(min(timeout_s, 300.0)))
+
+    def check():
+        probe = torch.ones(4, dtype=torch.float64, device=dev)
+        m.small_all_reduce_(st["h"], probe)
+        if float(probe[0].item()) != float(w):
+            raise RuntimeError(f"RCCL small communicator self-check failed ({probe[0].item()} != {w})")
+
+    def cleanup():
+        if st["h"]:
+            m.small_comm_abort(st["h"])
+            st["h"] = 0
+
+    ok, err = negotiate([draw, share, join, check], cleanup, group)
+    if not ok:
+        import logging
+        logging.warning(f"dedicated RCCL communicator unavailable ({err if err is not None else 'on a peer rank'})")
+        return 0
+    return st["h"]
 
 
 def small_all_reduce_(x: torch.Tensor, group=None) -> torch.Tensor:

@@ -11,9 +11,14 @@ reducer built on the flat gradient buffer of :class:`optim.flat.FlatParams`:
   backward keeps computing earlier layers;
 * averaging is not a separate pass: the optimizer kernel applies ``1/W`` (grad_scale)
   while it streams the gradients (``--grad_semantics exact`` keeps the sum);
-* bucket size defaults to 64 MiB: on a fully connected 8-GPU xGMI node each ring step is
-  bound by one 153 GB/s link, so fewer, larger buckets amortise per-collective latency
-  (the reference's 25 MB DDP default was sized for PCIe/NVLink rings);
+* bucket size defaults to 24 MiB (ResNet-50 + head: 112 MB of fp32 gradients -> 5
+  buckets). The constraint is overlap, not per-call latency: a bucket can only launch
+  when its last gradient exists, and the last bucket (layer 2/1 + stem) is exposed after
+  backward. With 64 MiB buckets the second (~48 MB) launched only at finish(); at 24 MiB
+  the layer-3 gradients go out while layer 2/1 are still in backward, leaving a few MB
+  for the tail. Per collective an 8-rank ring over xGMI moves 2(W-1)/W of the bucket
+  through one ~153 GB/s link per step, i.e. ≈0.3 ms for 24 MiB — well under the
+  backward time that follows each launch, and ≫ the ~20-40 µs fixed cost of a launch;
 * parameters/buffers are broadcast from rank 0 once at construction (one collective on
   the flat buffer); the per-forward BN buffer broadcast of DDP is dropped.
 """
@@ -28,7 +33,7 @@ from . import comm
 
 
 class GradBucketReducer:
-    def __init__(self, flat, bucket_mb: float = 64.0, group=None, enabled: Optional[bool] = None,
+    def __init__(self, flat, bucket_mb: float = 24.0, group=None, enabled: Optional[bool] = None,
                  broadcast_init: bool = True):
         self.flat = flat
         self.group = group
@@ -42,7 +47,7 @@ class GradBucketReducer:
             start = flat.offsets[i]
             end = start + (flat.params[i].numel() + 4095) // 4096 * 4096
             if cur is None or (end - cur["start"]) > cap and cur["params"]:
-                cur = {"start": start, "end": end, "params": [], "ready": 0, "work": None}
+                cur = {"start": start, "end": end, "params": [], "ready": 0, "work": None, "idx": len(self.buckets)}
                 self.buckets.append(cur)
             cur["params"].append(i)
             cur["end"] = end
@@ -60,6 +65,7 @@ class GradBucketReducer:
         self._seen = [False] * len(flat.params)
         self._paused = False
         self._listener = None
+        self.launch_log: List[int] = []     # bucket indices in launch order (tests, profiling)
         if self.enabled:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -102,13 +108,18 @@ class GradBucketReducer:
             ev = torch.cuda.current_stream().record_event()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
-                # fused blocks compute weight gradients on the wgrad side stream
+                # fused blocks compute weight gradients on the wgrad side stream. The hook
+                # fires right after the block that owns the bucket's last parameter issued
+                # its wgrads, and the side stream is FIFO, so this wait ends with that
+                # bucket's last wgrad — not behind wgrads of later (shallower) blocks.
                 from ..ops import streams
                 if streams.ENABLED:
                     self.comm_stream.wait_stream(streams.side(view.device))
                 b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+            self.launch_log.append(b["idx"])
         else:
             b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+            self.launch_log.append(b["idx"])
 
     def no_sync(self):
         """Context: gradients produced inside only accumulate locally (no bucket launches),

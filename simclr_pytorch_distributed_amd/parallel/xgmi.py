@@ -23,26 +23,45 @@ from ..ops import _ext
 
 
 class OneShotAllReduce:
-    def __init__(self, group=None, cap: int = 8192):
+    """Set-up runs as :func:`parallel.comm.negotiate` steps (create the arena, exchange
+    IPC handles, map the peers, self-check), with the ranks agreeing after each one: a
+    rank that fails to allocate or map raises on EVERY rank (after each rank destroyed
+    its own arena), never only on itself while its peers wait in a collective."""
+
+    def __init__(self, group=None, cap: int = 8192, timeout_s: float = 600.0):
+        from . import comm
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("process group not initialised")
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        if self.world > 8:
-            raise RuntimeError("one-shot xGMI all-reduce supports at most 8 ranks")
-        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
-        if lws != self.world:
-            raise RuntimeError("one-shot xGMI all-reduce needs every rank on one node")
         self.m = _ext.require()
         self.cap = cap
-        self.id = self.m.xgmi_create(self.rank, self.world, cap)
-        mine = bytes(self.m.xgmi_handle(self.id).numpy().tobytes())
-        allh = [None] * self.world
-        dist.all_gather_object(allh, mine, group=group)
-        h = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(self.world, 64).clone()
-        self.m.xgmi_open(self.id, h)
-        self._self_check()
+        self.id = None
+        st = {}
+
+        def check_topology():
+            if self.world > 8:
+                raise RuntimeError("one-shot xGMI all-reduce supports at most 8 ranks")
+            lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
+            if lws != self.world:
+                raise RuntimeError("one-shot xGMI all-reduce needs every rank on one node")
+
+        def create():
+            self.id = self.m.xgmi_create(self.rank, self.world, cap, float(timeout_s))
+            st["mine"] = bytes(self.m.xgmi_handle(self.id).numpy().tobytes())
+
+        def exchange():
+            allh = [None] * self.world
+            dist.all_gather_object(allh, st["mine"], group=group)
+            st["h"] = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(self.world, 64).clone()
+
+        def open_peers():
+            self.m.xgmi_open(self.id, st["h"])
+
+        ok, err = comm.negotiate([check_topology, create, exchange, open_peers, self._self_check], self.close, group)
+        if not ok:
+            raise RuntimeError(f"one-shot xGMI all-reduce unavailable ({err if err is not None else 'on a peer rank'})")
 
     def _self_check(self):
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -51,9 +70,7 @@ class OneShotAllReduce:
         torch.cuda.synchronize()
         err = self.m.xgmi_error(self.id)
         exp = torch.arange(16, dtype=torch.float64, device=dev) * self.world + 100.0 * sum(range(self.world))
-        ok = torch.tensor([1.0 if (err == 0 and torch.equal(out, exp)) else 0.0], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
-        if ok.item() != 1.0:
+        if not (err == 0 and torch.equal(out, exp)):
             raise RuntimeError(f"one-shot xGMI all-reduce self-check failed (err={err})")
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:

@@ -1,4 +1,4 @@
-"""Distributed semantics on CPU with gloo (world_size 2, multi-process).
+"""Distributed semantics on CPU with gloo (world sizes 2, 4 and 8, multi-process).
 
 * the row-owned distributed contrastive loss reproduces the single-process global loss
   (sum over ranks) and its exact gradient w.r.t. each rank's rows;
@@ -68,9 +68,10 @@ def _loss_case(rank, world, d, method):
     assert torch.allclose(loc.grad, g_ref, atol=1e-10)
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("method", ["SimCLR", "SupCon"])
-def test_distributed_loss_matches_global(method):
-    _run(_loss_case, 2, method)
+def test_distributed_loss_matches_global(method, world):
+    _run(_loss_case, world, method)
 
 
 # --------------------------------------------------------------------------------------
@@ -83,15 +84,15 @@ def _reducer_case(rank, world, d):
         return torch.nn.Sequential(torch.nn.Linear(64, 300), torch.nn.Linear(300, 500), torch.nn.Linear(500, 7))
 
     m, ref = make(), make()
-    if rank == 1:   # different init on rank 1: the reducer must broadcast rank 0's
+    if rank >= 1:   # different init on the other ranks: the reducer must broadcast rank 0's
         for p in m.parameters():
-            p.data.add_(1.0)
+            p.data.add_(float(rank))
     flat = FlatParams(m)
     red = GradBucketReducer(flat, bucket_mb=0.5)
     assert len(red.buckets) >= 2
     w0 = flat.flat.clone()
     dist.all_reduce(w0)
-    assert torch.allclose(w0, 2 * flat.flat)
+    assert torch.allclose(w0, world * flat.flat)
     x = torch.randn(5, 64) * (rank + 1)
     for _ in range(2):      # twice: the reducer must re-arm after finish()
         flat.zero_grad()
@@ -105,8 +106,9 @@ def _reducer_case(rank, world, d):
         assert torch.allclose(p.grad, g, rtol=1e-5, atol=1e-4)
 
 
-def test_bucket_reducer_matches_allreduce():
-    _run(_reducer_case, 2)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bucket_reducer_matches_allreduce(world):
+    _run(_reducer_case, world)
 
 
 # --------------------------------------------------------------------------------------
@@ -161,8 +163,9 @@ def _init_state():
 
 
 @pytest.mark.slow
-def test_two_rank_step_equals_single_rank():
-    _run(_step_case, 2)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_w_rank_step_equals_single_rank(world):
+    _run(_step_case, world)
 
 
 def _sink_case(rank, world, d):  # noqa: C901
@@ -232,3 +235,32 @@ def _gradcache_case(rank, world, d):
 
 def test_gradcache_two_ranks():
     _run(_gradcache_case, 2)
+
+
+def _overlap_case(rank, world, d):
+    """Reducer overlap: with the default bucket size, every bucket but
+    the last (the one holding the stem) is launched DURING backward, before the stem's
+    gradient exists — checked at the moment autograd accumulates the stem weight."""
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    from simclr_pytorch_distributed_amd.parallel.ddp import GradBucketReducer
+    torch.manual_seed(0)
+    m = SupConResNet("resnet50")
+    flat = FlatParams(m)
+    red = GradBucketReducer(flat)
+    nb = len(red.buckets)
+    assert nb >= 4, nb
+    seen = {}
+    stem = m.encoder.conv1.weight
+    stem.register_post_accumulate_grad_hook(lambda p: seen.setdefault("at_stem", list(red.launch_log)) and None)
+    x = torch.randn(4, 3, 32, 32)
+    flat.zero_grad()
+    m(x).square().mean().backward()
+    red.finish()
+    at = seen["at_stem"]
+    assert sorted(at) == list(range(nb - 1)) or sorted(at) == list(range(nb)), (at, nb)
+    assert len(at) >= nb - 1, (at, nb)
+
+
+def test_reducer_buckets_launch_during_backward():
+    _run(_overlap_case, 2)

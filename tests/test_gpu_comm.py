@@ -6,9 +6,9 @@ with a 1-rank communicator (linking against torch's librccl, ncclCommInitRank,
 ncclAllReduce on the compute stream), and the executor's cross-rank code path
 (reduce -> all-reduce -> finalize / coefficients) with the EMU kind: W virtual ranks that
 hold identical data, whose sum is x·W. SyncBN over W identical replicas must give the
-single-process statistics (so identical outputs, dx and conv weight gradients) while
-dγ/dβ — computed from the globally summed Σdz, Σdz·ŷ like the Python SyncBN path —
-come out ×W.
+single-process statistics (so identical outputs, dx and conv weight gradients) and the
+single-process dγ/dβ: each rank writes 1/W of the globally summed Σdz, Σdz·ŷ into its
+gradient sinks (its share; the bucket reducer's mean then gives torch's global / W).
 """
 import pytest
 import torch
@@ -94,7 +94,7 @@ def test_native_executor_syncbn_path(gpu, name, which):
     assert torch.allclose(b0.conv2.weight.grad, b1.conv2.weight.grad, rtol=1e-3, atol=1e-5)
     for n in ("bn1", "bn2"):
         g0, g1 = getattr(b0, n).weight.grad, getattr(b1, n).weight.grad
-        assert torch.allclose(W * g0, g1, rtol=1e-3, atol=1e-4), n
+        assert torch.allclose(g0, g1, rtol=1e-3, atol=1e-5), n
         g0, g1 = getattr(b0, n).bias.grad, getattr(b1, n).bias.grad
-        assert torch.allclose(W * g0, g1, rtol=1e-3, atol=1e-4), n
+        assert torch.allclose(g0, g1, rtol=1e-3, atol=1e-5), n
     m.small_comm_destroy(h)

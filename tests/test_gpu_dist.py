@@ -62,5 +62,14 @@ def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, syncbn_comm):
     rel = d_ref.norm() / (ref["flat"].norm() + 1e-12)
     assert rel < 2e-3, float(rel)
     assert torch.allclose(a["rm"], ref["rm"], rtol=1e-2, atol=1e-3)
+    # per-parameter gradient of the W=2 step vs the W=1 step on the same global batch
+    # (exact semantics: the reducer sums). BatchNorm γ/β are checked like every conv:
+    # a rank that wrote the all-reduced dγ instead of its share would be off by ×W.
+    worst = []
+    for n, o, k in zip(a["names"], a["offsets"], a["numels"]):
+        g1, g2 = ref["grad"][o:o + k].double(), a["grad"][o:o + k].double()
+        worst.append((float((g2 - g1).norm() / (g1.norm() + 1e-12)), n))
+    worst.sort(reverse=True)
+    assert worst[0][0] < 5e-2, worst[:8]
     # global loss = sum of the ranks' row-owned losses
     assert abs(a["loss"] + b["loss"] - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3

@@ -137,3 +137,33 @@ def test_native_engine_step_imagenet_supcon_lars(gpu, tmp_path):
     assert all(torch.isfinite(torch.tensor(losses)))
     assert not torch.equal(w0, eng.flat.flat)
     assert torch.isfinite(eng.flat.flat).all().item()
+
+
+def test_cuda_graph_follows_eager_trajectory(gpu, tmp_path):
+    """--cuda_graph: the capture warm-up steps are undone, so a graphed run
+    makes exactly the eager run's updates: same parameters after 3 steps on the same
+    batches (up to run-to-run reduction-order noise of the split-K/atomic kernels)."""
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    res = []
+    for graph in (False, True):
+        opt = parse_pretrain(["--batch_size", "32", "--synthetic", "--synthetic_size", "128", "--work_dir",
+                              str(tmp_path / f"g{int(graph)}"), "--model", "resnet18", "--backend", "native",
+                              "--learning_rate", "0.05", "--seed", "3"], make_dirs=False)
+        eng = PretrainEngine(opt)
+        torch.manual_seed(11)
+        from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+        eng.model.load_state_dict(SupConResNet("resnet18").state_dict())
+        idx = torch.arange(32, device=gpu)
+        if graph:
+            assert eng.enable_cuda_graph(idx)
+        w_init = eng.flat.flat.clone()
+        for it in range(3):
+            eng.train_step(idx, 1, it, 10)
+        torch.cuda.synchronize()
+        res.append((w_init, eng.flat.flat.clone(), eng.model.encoder.bn1.running_mean.clone()))
+    (i0, w0, r0), (i1, w1, r1) = res
+    assert torch.equal(i0, i1), "graph warm-up updates were not undone"
+    rel = float((w0 - w1).norm() / (w0 - i0).norm())
+    assert rel < 2e-2, rel
+    assert torch.allclose(r0, r1, rtol=1e-3, atol=1e-4)
