@@ -11,6 +11,16 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 la
 with torch.distributed.run, one rank per GPU. W untimed steps, then exactly K steps
 bracketed by barrier + synchronize; the time is the MAX over ranks; rank 0 prints one
 JSON line. ``value`` = whole-job source images/sec (each image is processed as 2 views).
+
+Other BASELINE.json configs (same step, same JSON line):
+
+* ``--global_batch 256`` on 2 GPUs: the README headline config (BS 256 over 2 ranks,
+  128 per GPU, strong scaling); ``--per_gpu_batch 128`` is its 1-GPU slice.
+* ``--dataset cifar100 --global_batch 1024``: config 4 (8 GPUs, 128 per GPU).
+* ``--config supcon224``: config 5 — SupCon, ImageNet stem at 224x224, LARS, 512 images
+  (1024 views) per GPU by default, encoder passes in gradient-cache chunks of
+  ``--micro_batch`` views (BN statistics per chunk, parallel/gradcache notes in
+  engine/pretrain.py); reports peak HBM against the 288 GB of one MI355X.
 """
 from __future__ import annotations
 
@@ -32,7 +42,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--per_gpu_batch", type=int, default=256)
+    ap.add_argument("--per_gpu_batch", type=int, default=None,
+                    help="images per GPU (weak scaling; default 256, 512 for --config supcon224)")
+    ap.add_argument("--global_batch", type=int, default=None,
+                    help="fixed total images per step split over the ranks (strong scaling)")
+    ap.add_argument("--dataset", default="cifar10", choices=["cifar10", "cifar100"])
+    ap.add_argument("--config", default="simclr32", choices=["simclr32", "supcon224"])
+    ap.add_argument("--micro_batch", type=int, default=None,
+                    help="views per encoder chunk (gradient cache); default: whole batch, 256 for supcon224")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--no_syncbn", action="store_true")
@@ -51,12 +68,26 @@ def main():
     if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     n = world
-    global_batch = a.per_gpu_batch * n
+    big = a.config == "supcon224"
+    if a.global_batch is not None:
+        if a.global_batch % n:
+            raise SystemExit(f"--global_batch {a.global_batch} is not divisible by {n} ranks")
+        per_gpu, scaling = a.global_batch // n, "strong"
+    else:
+        per_gpu, scaling = (a.per_gpu_batch or (512 if big else 256)), "weak"
+    global_batch = per_gpu * n
     work = os.path.join(tempfile.gettempdir(), f"sdx_bench_{os.getpid()}")
-    argv = ["--batch_size", str(global_batch), "--model", a.model, "--temp", "0.5", "--learning_rate", "0.5",
-            "--cosine", "--method", "SimCLR", "--epochs", "100", "--synthetic",
-            "--synthetic_size", str(max(8192, 4 * global_batch)), "--backend", a.backend,
+    size = 224 if big else 32
+    argv = ["--batch_size", str(global_batch), "--model", a.model, "--temp", "0.5" if not big else "0.1",
+            "--learning_rate", "0.5", "--cosine", "--method", "SupCon" if big else "SimCLR", "--epochs", "100",
+            "--synthetic", "--synthetic_size", str(max(2 * global_batch if big else 8192, 4 * per_gpu)),
+            "--backend", a.backend, "--dataset", a.dataset,
             "--work_dir", work, "--print_freq", "1000000", "--ngpu", str(n)]
+    if big:
+        argv += ["--stem", "imagenet", "--size", "224", "--optimizer", "lars"]
+    mb = a.micro_batch if a.micro_batch is not None else (256 if big else 0)
+    if mb:
+        argv += ["--micro_batch", str(mb)]
     if n > 1 and not a.no_syncbn:
         argv.append("--syncBN")
     opt = parse_pretrain(argv + extra, make_dirs=False)
@@ -116,16 +147,24 @@ def main():
     ms = dt / a.steps * 1e3
     value = global_batch * a.steps / dt
     d_in = {"resnet18": 512, "resnet34": 512}.get(a.model, 2048)
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else 0.0
+    if big:
+        desc = f"{a.model} (ImageNet stem, 224x224) + MLP head {d_in}-{d_in}-128, SupCon tau=0.1, LARS"
+        metric = METRIC.replace("SimCLR ResNet-50 BS=256", "SupCon ResNet-50 224x224")
+    else:
+        desc = f"{a.model} (CIFAR stem) + MLP head {d_in}-{d_in}-128, SimCLR tau=0.5"
+        metric = METRIC
     if comm.rank() == 0:
         print(json.dumps({
-            "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "metric": metric, "value": round(value, 2), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"model": f"{a.model} (CIFAR stem) + MLP head {d_in}-{d_in}-128, SimCLR tau=0.5",
-                       "global_batch": global_batch, "per_gpu_batch": a.per_gpu_batch, "views": 2,
-                       "image_size": 32, "seq_len": None,
+            "config": {"model": desc, "dataset_shape": a.dataset,
+                       "global_batch": global_batch, "per_gpu_batch": per_gpu, "views": 2,
+                       "image_size": size, "seq_len": None, "micro_batch_views": mb or None,
                        "parallelism": f"dp{n}" + ("+syncbn" if n > 1 and not a.no_syncbn else ""),
                        "backend": eng.backend, "hip_graph": graphed, "views_per_sec": round(2 * value, 2),
+                       "peak_hbm_gb": round(peak_gb, 2), "hbm_capacity_gb": 288,
                        "last_loss_local": round(loss, 4)},
         }), flush=True)
     if dist.is_initialized():

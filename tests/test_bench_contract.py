@@ -37,3 +37,18 @@ def test_bench_two_ranks_json_contract(tmp_path):
     assert c["global_batch"] == 8 and c["per_gpu_batch"] == 4 and c["parallelism"] == "dp2+syncbn"
     # value = whole-job images/s = global batch x steps / time
     assert abs(d["value"] - 8 * 1e3 / d["ms_per_step"]) / d["value"] < 0.01
+
+
+def test_bench_global_batch_is_strong_scaling(tmp_path):
+    """--global_batch fixes the total batch (README headline: BS 256 over 2 GPUs)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--backend", "torch", "--model", "resnet18",
+           "--global_batch", "8", "--dataset", "cifar100"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["scaling"] == "strong"
+    assert d["config"]["global_batch"] == 8 and d["config"]["per_gpu_batch"] == 4
+    assert d["config"]["dataset_shape"] == "cifar100"
