@@ -18,9 +18,10 @@ Other BASELINE.json configs (same step, same JSON line):
   128 per GPU, strong scaling); ``--per_gpu_batch 128`` is its 1-GPU slice.
 * ``--dataset cifar100 --global_batch 1024``: config 4 (8 GPUs, 128 per GPU).
 * ``--config supcon224``: config 5 — SupCon, ImageNet stem at 224x224, LARS, 512 images
-  (1024 views) per GPU by default, encoder passes in gradient-cache chunks of
-  ``--micro_batch`` views (BN statistics per chunk, parallel/gradcache notes in
-  engine/pretrain.py); reports peak HBM against the 288 GB of one MI355X.
+  (1024 views) per GPU: the whole local batch in ONE encoder pass (full-batch BN
+  semantics, as the reference recipe) — it needs ≈51 GB of the 288 GB of HBM, measured
+  (profiles/cfg5_slice_r2.json). ``--micro_batch V`` switches to gradient-cache chunks
+  of V views (per-chunk BN statistics, see engine/pretrain.py) for larger batches.
 """
 from __future__ import annotations
 
@@ -48,8 +49,8 @@ def main():
                     help="fixed total images per step split over the ranks (strong scaling)")
     ap.add_argument("--dataset", default="cifar10", choices=["cifar10", "cifar100"])
     ap.add_argument("--config", default="simclr32", choices=["simclr32", "supcon224"])
-    ap.add_argument("--micro_batch", type=int, default=None,
-                    help="views per encoder chunk (gradient cache); default: whole batch, 256 for supcon224")
+    ap.add_argument("--micro_batch", type=int, default=0,
+                    help="views per encoder chunk (gradient cache); 0 = the whole local batch in one pass")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--no_syncbn", action="store_true")
@@ -85,7 +86,7 @@ def main():
             "--work_dir", work, "--print_freq", "1000000", "--ngpu", str(n)]
     if big:
         argv += ["--stem", "imagenet", "--size", "224", "--optimizer", "lars"]
-    mb = a.micro_batch if a.micro_batch is not None else (256 if big else 0)
+    mb = a.micro_batch
     if mb:
         argv += ["--micro_batch", str(mb)]
     if n > 1 and not a.no_syncbn:
