@@ -60,7 +60,10 @@ def init_distributed(backend_name: str = "auto", timeout_s: float = 600.0, devic
         if backend_name == "auto":
             backend_name = "nccl" if device.type == "cuda" else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        kw = dict(backend=backend_name, init_method="env://", world_size=world, rank=rnk,
+        # SDX_INIT_METHOD (e.g. file:///tmp/rdv): a port-free rendezvous for tests that
+        # start ranks on a shared box, where a probed free port can be taken before use
+        init = os.environ.get("SDX_INIT_METHOD", "env://")
+        kw = dict(backend=backend_name, init_method=init, world_size=world, rank=rnk,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend_name == "nccl":
             kw["device_id"] = device

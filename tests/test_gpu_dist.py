@@ -4,7 +4,6 @@ with gathered negatives, bucketed gradient reduction on the comm stream, fused S
 must reproduce the single-rank step on the concatenated batch (exact gradient
 semantics), up to bf16 reduction-order noise."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -15,20 +14,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _launch(world, out, syncbn_comm=""):
-    port = _free_port()
+    # file-store rendezvous: no probed TCP port that another job on the box can take first
+    rdv = os.path.join(str(out), f"rdv_{world}_{syncbn_comm or 'pg'}")
     procs = []
     for r in range(world):
-        env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+        env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD="file://" + rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     for p in procs:

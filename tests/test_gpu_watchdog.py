@@ -10,7 +10,6 @@
   status 3 and one clear line instead of hanging or training on stale statistics.
 """
 import os
-import socket
 import subprocess
 import sys
 import time
@@ -48,20 +47,12 @@ def test_watchdog_ends_a_stalled_collective(gpu):
     assert "did not complete within 1.0 s" in p.stderr
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 def test_xgmi_stalled_peer_exits_3(gpu, tmp_path):
-    port = _free_port()
+    rdv = "file://" + str(tmp_path / "rdv")
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT, OMP_NUM_THREADS="4",
+                   MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD=rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4",
                    SDX_FAULT_INJECT="rank=1,step=1,mode=hang,seconds=90")
         cmd = [sys.executable, os.path.join(ROOT, "main_supcon.py"), "--model", "resnet18", "--batch_size", "16",
                "--synthetic", "--synthetic_size", "64", "--epochs", "1", "--print_freq", "1", "--backend", "native",
