@@ -1,6 +1,7 @@
 // Bindings for the implicit-GEMM convolution (igemm.hip) and BatchNorm (bn.hip) kernels.
 // Host-side shape/dtype/layout checks run before every launch.
 #include "ops_decl.h"
+#include "conv_internal.h"
 #include "launchers.h"
 
 #include <c10/hip/HIPCachingAllocator.h>
@@ -12,7 +13,6 @@
 #include <mutex>
 
 namespace sdx_bind {
-namespace {
 
 using OptT = c10::optional<torch::Tensor>;
 
@@ -49,7 +49,7 @@ void in_bn_ptrs(const OptT& sc, const OptT& sh, int64_t C, const float** ps, con
 // two-per-CU slots). The small 64x64 tile is only penalised when the GEMM is
 // compute-bound (long K); short-K (memory-bound) GEMMs favour its higher occupancy.
 // Calibrated with tools/conv_bench.py --cfg 0..3 on the ResNet-50 shapes.
-int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim = 0, bool fill = false) {
+int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
   const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
   const bool long_k = Kdim == 0 || Kdim > 256;
   const double pen_long[4] = {1.0, 1.04, 1.04, 1.35}, pen_short[4] = {1.0, 1.0, 1.0, 1.05};
@@ -74,6 +74,8 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim = 0, bool fill = false) {
   if (fill && best == 0 && Kdim >= 128) best = 4;
   return best;
 }
+
+namespace {
 
 std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
                                     int64_t cfg, OptT in_scale, OptT in_shift) {
@@ -239,6 +241,8 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
   return {dx, slab};
 }
 
+}  // namespace
+
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                          int64_t splits, int64_t cfg, c10::optional<torch::Tensor> out, bool accumulate,
                          OptT in_scale, OptT in_shift) {
@@ -326,6 +330,8 @@ void check_slab(const torch::Tensor& slab, int64_t nsets) {
 torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t nsets, int64_t C) {
   return torch::empty({col_reduce_gy((int)rows) * nsets * C}, like.options().dtype(at::kDouble));
 }
+
+namespace {
 
 torch::Tensor bn_stats_reduce(torch::Tensor slab) {
   check_slab(slab, 2);

@@ -10,6 +10,7 @@ void register_pool(pybind11::module& m);
 void register_wprep(pybind11::module& m);
 void register_xgmi(pybind11::module& m);
 void register_comm(pybind11::module& m);
+void register_head(pybind11::module& m);
 
 void register_ops(pybind11::module& m) {
   register_supcon(m);
@@ -20,5 +21,6 @@ void register_ops(pybind11::module& m) {
   register_wprep(m);
   register_xgmi(m);
   register_comm(m);
+  register_head(m);
 }
 }  // namespace sdx_bind

@@ -49,18 +49,28 @@ struct BnBwdStat {
   const float* msc;
   const float* msh;
   int row0;
+  int store_masked;      // store dx·m instead of dx (ReLU backward fused into the store)
+};
+// plain-GEMM epilogue of FWD / DGRAD launches (projection head): per-column fp32 bias,
+// ReLU, fp32 output (stride-1 geometry, no BN statistics / addend with out_f32)
+struct GemmEpi {
+  const float* bias;
+  int relu;
+  int out_f32;
 };
 int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
-                           hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr);
+                           hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr,
+                           const GemmEpi* epi = nullptr);
 // strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous)
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
-                                   const BnBwdStat* bstat = nullptr, int addend_sub = 0);
+                                   const BnBwdStat* bstat = nullptr, int addend_sub = 0,
+                                   const GemmEpi* epi = nullptr);
 // M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
 int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
@@ -96,7 +106,8 @@ struct BnCoefArgs {
 };
 // Deterministic reduction of a [rows][nsets][C] fp32 slab to fp64 sums [nsets][C] in ONE
 // launch (per-block partials + last-arriver combine; no memset). epi: 0 sums only,
-// 1 + BN finalize (nsets 2), 2 + BN backward coefficients (nsets 2|3).
+// 1 + BN finalize (nsets 2), 2 + BN backward coefficients (nsets 2|3), 3 gradient-sink add
+// of set 0 (ca->dbeta_a[c] += Σ·ca->grad_scale: a bias gradient; nsets 1|2).
 int col_reduce_gy(int rows);
 hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, double* scratch, unsigned* counters,
                              double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s);

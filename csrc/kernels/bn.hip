@@ -165,8 +165,9 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
     for (int q = 0; q < NS; ++q) t[q] = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
 #pragma unroll
     for (int q = 0; q < NS; ++q) sums[(size_t)q * C + c] = t[q];
-    if (EPI == 1) bn_finalize_one(c, t[0], t[1], fa);
-    if (EPI == 2) bn_coef_one(c, C, t, NS - 1, ca);
+    if constexpr (EPI == 1) bn_finalize_one(c, t[0], t[1], fa);
+    if constexpr (EPI == 2) bn_coef_one(c, C, t, NS - 1, ca);
+    if constexpr (EPI == 3) ca.dbeta_a[c] += (float)(t[0] * ca.grad_scale);
   }
   if (gy > 1 && threadIdx.x == 0) __hip_atomic_store(counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -485,14 +486,17 @@ int col_reduce_gy(int rows) {
 
 hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, double* scratch, unsigned* counters,
                              double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s) {
-  if (rows < 1 || C < 1 || (epi == 1 && (nsets != 2 || !fa)) || (epi == 2 && (nsets < 2 || !ca)))
+  if (rows < 1 || C < 1 || (epi == 1 && (nsets != 2 || !fa)) || (epi == 2 && (nsets < 2 || !ca)) ||
+      (epi == 3 && (nsets > 2 || !ca || !ca->dbeta_a)) || (nsets == 1 && epi != 0 && epi != 3))
     return hipErrorInvalidValue;
   const dim3 grid((C + 63) / 64, col_reduce_gy(rows)), blk(256);
   const BnFinalizeArgs f = fa ? *fa : BnFinalizeArgs{};
   const BnCoefArgs k = ca ? *ca : BnCoefArgs{};
 #define SDX_CR(NS, EPI) hipLaunchKernelGGL((col_reduce_kernel<NS, EPI>), grid, blk, 0, s, slab, rows, C, scratch, counters, sums, f, k)
-  if (nsets == 2) {
-    if (epi == 0) SDX_CR(2, 0); else if (epi == 1) SDX_CR(2, 1); else SDX_CR(2, 2);
+  if (nsets == 1) {
+    if (epi == 0) SDX_CR(1, 0); else SDX_CR(1, 3);
+  } else if (nsets == 2) {
+    if (epi == 0) SDX_CR(2, 0); else if (epi == 1) SDX_CR(2, 1); else if (epi == 2) SDX_CR(2, 2); else SDX_CR(2, 3);
   } else if (nsets == 3) {
     if (epi == 0) SDX_CR(3, 0); else SDX_CR(3, 2);
   } else {

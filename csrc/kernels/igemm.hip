@@ -72,6 +72,11 @@ struct IgemmParams {
   long a_elems, b_elems;
   // DGRAD: fused BN-backward statistics of the stored output (BnBwdStat; bs.slab null = off)
   BnBwdStat bs;
+  // FWD / DGRAD plain-GEMM epilogue (projection head, csrc/bindings/head_ops.cpp): optional
+  // per-output-column fp32 bias and ReLU on the fp32 accumulators; out_f32 = fp32 output
+  // rows stored straight from the accumulators (no bf16 rounding, no BN statistics)
+  const float* bias;
+  int relu, out_f32;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -166,12 +171,12 @@ struct Tile {
 // (global_load_lds) staging of both K-inner operands (FWD / DGRAD without the BN prologue):
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
-// BST (DGRAD only): fused BN-backward statistics epilogue (p.bs) — a separate variant so
+// BST (DGRAD only): 1 = fused BN-backward statistics epilogue (p.bs) — a separate variant so
 // the plain dgrad keeps its register budget. ONE (LDS-DMA, reduction <= BK): a single
 // K-tile needs no second LDS buffer; the smaller static LDS (one stage or the C tile) lets
 // twice as many blocks share a CU, hiding the load -> MFMA -> store latency of these
 // memory-bound 1x1 layer-1 GEMMs across blocks.
-template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, bool BST, bool ONE>
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int BST, bool ONE>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
   using T = Tile<MODE, BM, BN, NT>;
@@ -744,8 +749,26 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 
   // ---------------------------------- epilogues ----------------------------------
   // acc[i][j][r] = C[m0 + wm*64 + 16i + c][n0 + wn*64 + 16j + 4h + r]
-  if (MODE == MODE_WGRAD) {
-    float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.M * p.Ncol;
+  // (not compiled into the BN-statistics DGRAD variant: its register budget sits at the
+  // 128-VGPR occupancy step)
+  if (MODE != MODE_WGRAD && !BST && (p.bias != nullptr || p.relu)) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wn * WTN + 16 * j + 4 * h + r;
+        const float b = (p.bias != nullptr && col < p.Ncol) ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float v = acc[i][j][r] + b;
+          acc[i][j][r] = p.relu ? fmaxf(v, 0.f) : v;
+        }
+      }
+  }
+  if (MODE == MODE_WGRAD || (!BST && p.out_f32)) {
+    // fp32 rows straight from the accumulators: 4 consecutive columns per lane (WGRAD: this
+    // split's partial slab; FWD / DGRAD out_f32: stride-1 GEMM rows, host-checked)
+    float* out = reinterpret_cast<float*>(p.out) + (MODE == MODE_WGRAD ? (size_t)split * p.M * p.Ncol : 0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = m0 + wm * WTM + 16 * i + c;
@@ -779,7 +802,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int PF = ITER < 4 ? ITER : 4;
   static_assert(NT % CPR == 0 && CPR <= 64 && (BM * CPR) % NT == 0, "fixed column chunk per thread");
   const bool has_add = MODE == MODE_DGRAD && p.addend != nullptr;
-  constexpr bool bst = MODE == MODE_DGRAD && BST;
+  constexpr bool bst = MODE == MODE_DGRAD && BST != 0;
   const int my_ch = tid % CPR, my_col = n0 + my_ch * 8;
   int eo[ITER];   // output element offset of each chunk (-1: outside the tensor)
   int ea[ITER];   // addend element offset (-1: no addend there)
@@ -912,6 +935,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) d[q] = ya[q] * bmk_s[q] + bmk_t[q] > 0.f ? d[q] : 0.f;
           }
+          // BST 2: ReLU backward applied to the stored gradient too (head: dh = (dz·W2)·[h > 0]):
+          // the chunk is stored again, masked (bf16 values already, so the repack is exact).
+          // Its own variant: the BN-statistics kernels sit at the 128-VGPR occupancy step
+          if constexpr (BST == 2) *reinterpret_cast<uint4*>(out + o) = pack8(d);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             bsum[0][q] += d[q];
@@ -1081,24 +1108,33 @@ int igemm_one() {
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   const dim3 g(grid), b(64 * WM * WN);
+  if (bs && p.bs.store_masked) {
+    // masked-store statistics variant (projection head): 64x64 LDS-DMA tiles only
+    if constexpr (MODE == MODE_DGRAD && BM == 64 && BN == 64 && DEPTH == 3) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, false>), g, b, 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+    return hipErrorInvalidValue;
+  }
   if constexpr (DEPTH == 3 && MODE != MODE_WGRAD) {
     if (p.Kdim <= BK && igemm_one()) {
       if (MODE == MODE_DGRAD && bs)
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, MODE == MODE_DGRAD, true>), g, b, 0, s, p);
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, MODE == MODE_DGRAD ? 1 : 0, true>), g, b, 0, s, p);
       else
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, false, true>), g, b, 0, s, p);
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 0, true>), g, b, 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
   }
   if constexpr (MODE == MODE_DGRAD) {
     if (bs) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, true, false>), g, b, 0, s, p);
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 1, false>), g, b, 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
   }
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, false, false>), g, b, 0, s, p);
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 0, false>), g, b, 0, s, p);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1125,7 +1161,7 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   }
   if constexpr (kDepth2) {
     if (igemm_depth() == 2 && !bs) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2, false, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2, 0, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
@@ -1160,9 +1196,20 @@ int igemm_tile_n(int cfg) {
   return n[cfg];
 }
 
+namespace {
+void set_epi(IgemmParams& p, const GemmEpi* epi) {
+  if (epi == nullptr) return;
+  p.bias = epi->bias;
+  p.relu = epi->relu;
+  p.out_f32 = epi->out_f32;
+}
+}  // namespace
+
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
-                           hipStream_t s, const float* in_scale, const float* in_shift) {
+                           hipStream_t s, const float* in_scale, const float* in_shift, const GemmEpi* epi) {
   IgemmParams p{};
+  set_epi(p, epi);
+  if (p.out_f32 && stats != nullptr) return hipErrorInvalidValue;
   p.in_scale = in_scale;
   p.in_shift = in_shift;
   p.g = g;
@@ -1197,8 +1244,11 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
-                                   const BnBwdStat* bstat, int addend_sub) {
+                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi) {
   IgemmParams p{};
+  set_epi(p, epi);
+  if (p.out_f32 && (g.stride != 1 || addend != nullptr || (bstat != nullptr && bstat->slab != nullptr)))
+    return hipErrorInvalidValue;
   p.addend_sub = addend_sub;
   if (bstat != nullptr) p.bs = *bstat;
   p.addend_mask = (const uint8_t*)addend_mask;

@@ -96,3 +96,51 @@ def test_native_head_matches_autograd(gpu, head):
     for pa, pb in zip(a.head.parameters(), b.head.parameters()):
         assert pa.grad is not None
         assert rel(pa.grad, pb.grad) < 1e-2
+
+
+@pytest.mark.parametrize("rows,din,dout,head", [(77, 512, 64, "mlp"), (256, 2048, 128, "mlp"), (40, 256, 128, "linear")])
+def test_native_head_vs_fp32(gpu, rows, din, dout, head):
+    """Hand-written head GEMMs (igemm 1x1 + fused bias/ReLU/fp32 epilogues, ReLU-backward
+    store + bias column sums) vs a plain fp32 torch autograd reference of the same head."""
+    import torch.nn as nn
+    from simclr_pytorch_distributed_amd.ops.head import projection_head
+    from simclr_pytorch_distributed_amd.ops.weights import ConvWeightCache
+    torch.manual_seed(3)
+    if head == "mlp":
+        mod = nn.Sequential(nn.Linear(din, din), nn.ReLU(inplace=True), nn.Linear(din, dout)).to(gpu)
+        with torch.no_grad():
+            for lin in (mod[0], mod[2]):
+                lin.bias.uniform_(-0.5, 0.5)   # biases large enough to matter
+    else:
+        mod = nn.Linear(din, dout).to(gpu)
+    ref = __import__("copy").deepcopy(mod)
+    lins = [m for m in mod.modules() if isinstance(m, nn.Linear)]
+    wc = ConvWeightCache(lins, None)
+    wc.refresh()
+    feat = torch.randn(rows, din, device=gpu)
+    fa = feat.clone().requires_grad_(True)
+    fr = feat.clone().requires_grad_(True)
+    ac = __import__("copy").deepcopy(mod)
+    fc = feat.clone().requires_grad_(True)
+    za = projection_head(fa, mod, wc)
+    zr = ref(fr)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        zc = ac(fc).float()
+    rel = lambda u, v: ((u.double() - v.double()).norm() / v.double().norm().clamp_min(1e-12)).item()  # noqa: E731
+    # error budget: torch's own bf16 autocast of the same head against fp32 (the ReLU mask
+    # flips at near-zero hidden units dominate the backward), with 1.5x slack and a floor
+    env = lambda a, c, r: max(1.5 * rel(c, r), 4e-3)  # noqa: E731
+    assert za.dtype == torch.float32 and za.shape == zr.shape
+    assert rel(za, zr) < env(za, zc, zr), (rel(za, zr), rel(zc, zr))
+    g = torch.randn_like(za)
+    za.backward(g)
+    zr.backward(g)
+    zc.backward(g)
+    assert rel(fa.grad, fr.grad) < env(fa.grad, fc.grad, fr.grad), (rel(fa.grad, fr.grad), rel(fc.grad, fr.grad))
+    for (n, pa), pr, pc in zip(mod.named_parameters(), ref.parameters(), ac.parameters()):
+        assert rel(pa.grad, pr.grad) < env(pa.grad, pc.grad, pr.grad), (n, rel(pa.grad, pr.grad), rel(pc.grad, pr.grad))
+    # gradients accumulate into the sinks (a second backward doubles them)
+    g1 = [p.grad.clone() for p in mod.parameters()]
+    projection_head(feat.clone().requires_grad_(True), mod, wc).backward(g)
+    for p, a in zip(mod.parameters(), g1):
+        assert torch.allclose(p.grad, 2 * a, rtol=1e-5, atol=1e-6)
