@@ -90,6 +90,8 @@ def test_fused_blocks_match_unfused(gpu, name, variant, monkeypatch):
     from simclr_pytorch_distributed_amd.ops import block
     monkeypatch.setattr(block, "FUSE_PROLOGUE", variant == "py_prologue")
     monkeypatch.setattr(block, "NATIVE_EXEC", variant == "native_exec")
+    from simclr_pytorch_distributed_amd.models import executor
+    monkeypatch.setattr(executor, "FUSED_HEAD", False)   # same (torch) head on both sides
     from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
     from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams
