@@ -329,6 +329,116 @@ void small_comm_stall_(int64_t h, double seconds, torch::Tensor x) {
 
 int64_t small_comm_ops(int64_t h) { return get(h)->ops.load(); }
 
+// 0 none, 1 RCCL, 2 xGMI, 3 emulated
+int64_t small_comm_kind(int64_t h) { return h == 0 ? 0 : (int64_t)get(h)->kind; }
+int64_t small_comm_rank(int64_t h) { return h == 0 ? 0 : (int64_t)get(h)->rank; }
+
+ncclDataType_t nccl_type(const torch::Tensor& x, const char* what) {
+  switch (x.scalar_type()) {
+    case at::kDouble: return ncclFloat64;
+    case at::kFloat: return ncclFloat32;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    default: TORCH_CHECK(false, what, ": fp64 / fp32 / int32 / int64 only");
+  }
+}
+
+SmallComm& gather_comm(int64_t h, const torch::Tensor& x, const char* what) {
+  SmallComm& c = *get(h);
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.device().index() == c.device, what,
+              ": contiguous tensor on the communicator's device");
+  TORCH_CHECK(c.kind == KIND_RCCL || c.kind == KIND_EMU, what, ": RCCL or emulated communicator only");
+  if (c.kind == KIND_RCCL) TORCH_CHECK(c.nccl, what, ": RCCL communicator was aborted");
+  return c;
+}
+
+// in place: rows [rank·n, (rank+1)·n) of `out` ([W·n, ...]) hold this rank's block on entry;
+// on exit every block holds its rank's rows. Emulated ranks are identical: block copies.
+void all_gather_inplace(SmallComm& c, torch::Tensor& out, int64_t block_elems) {
+  if (c.world == 1 && c.kind != KIND_RCCL) return;   // (a 1-rank RCCL call is a tested no-op)
+  hipStream_t s = cur_stream();
+  const int64_t bytes = block_elems * out.element_size();
+  char* base = static_cast<char*>(out.data_ptr());
+  if (c.kind == KIND_RCCL) {
+    settle(c, ncclAllGather(base + c.rank * bytes, base, (size_t)block_elems, nccl_type(out, "all-gather"), c.nccl, s),
+           "ncclAllGather");
+  } else {
+    for (int r = 0; r < c.world; ++r)
+      if (r != c.rank)
+        check_hip(hipMemcpyAsync(base + r * bytes, base + c.rank * bytes, bytes, hipMemcpyDeviceToDevice, s),
+                  "emulated all-gather");
+  }
+  arm(c, s);
+}
+
+// x [n, ...] -> [W·n, ...] (rank-major), ordered on the current stream
+torch::Tensor small_all_gather(int64_t h, torch::Tensor x) {
+  SmallComm& c = gather_comm(h, x, "small all-gather");
+  auto sizes = x.sizes().vec();
+  sizes[0] *= c.world;
+  auto out = torch::empty(sizes, x.options());
+  out.narrow(0, c.rank * x.size(0), x.size(0)).copy_(x);
+  all_gather_inplace(c, out, x.numel());
+  return out;
+}
+
+// g [W·n, ...] -> Σ_ranks g[rank block] ([n, ...]) (emulated: W identical ranks -> W·g[block])
+torch::Tensor small_reduce_scatter(int64_t h, torch::Tensor g) {
+  SmallComm& c = gather_comm(h, g, "small reduce-scatter");
+  TORCH_CHECK(g.size(0) % c.world == 0, "small reduce-scatter: rows not divisible by the world size");
+  const int64_t n = g.size(0) / c.world;
+  auto sizes = g.sizes().vec();
+  sizes[0] = n;
+  if (c.world == 1 && c.kind != KIND_RCCL) return g.clone();
+  hipStream_t s = cur_stream();
+  torch::Tensor out;
+  if (c.kind == KIND_RCCL) {
+    out = torch::empty(sizes, g.options());
+    settle(c, ncclReduceScatter(g.data_ptr(), out.data_ptr(), (size_t)out.numel(), nccl_type(g, "reduce-scatter"),
+                                ncclSum, c.nccl, s),
+           "ncclReduceScatter");
+  } else {
+    out = g.narrow(0, c.rank * n, n).mul((double)c.world);
+  }
+  arm(c, s);
+  return out;
+}
+
+// Contrastive-loss input: L2-normalise this rank's projections straight
+// into its block of the gathered contrast matrix, then all-gather in place — the loss
+// kernel reads the result directly. Returns (C [W·n, d] fp32, row norms [n]).
+std::vector<torch::Tensor> rownorm_gather(int64_t h, torch::Tensor x, double eps) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 2 && x.is_contiguous() && x.size(1) <= 256,
+              "rownorm_gather: contiguous fp32 [n, d <= 256]");
+  SmallComm& c = gather_comm(h, x, "rownorm_gather");
+  c10::DeviceGuard dg(x.device());
+  const int64_t n = x.size(0), d = x.size(1);
+  auto C = torch::empty({c.world * n, d}, x.options());
+  auto norms = torch::empty({n}, x.options());
+  float* mine = C.data_ptr<float>() + c.rank * n * d;
+  check_hip(launch_rownorm_fwd(x.data_ptr<float>(), (int)n, (int)d, (float)eps, mine, norms.data_ptr<float>(),
+                               cur_stream()),
+            "rownorm_fwd");
+  all_gather_inplace(c, C, n * d);
+  return {C, norms};
+}
+
+// backward of rownorm_gather: reduce-scatter the contrast-matrix gradient to the owners,
+// then the row-normalisation gradient. y: this rank's normalised rows (C's block).
+torch::Tensor rownorm_gather_bwd(int64_t h, torch::Tensor gC, torch::Tensor y, torch::Tensor norms, double eps) {
+  TORCH_CHECK(gC.is_cuda() && gC.scalar_type() == at::kFloat && gC.dim() == 2, "gC: fp32 [W·n, d]");
+  gC = gC.contiguous();
+  y = y.contiguous();
+  c10::DeviceGuard dg(gC.device());
+  auto g = small_reduce_scatter(h, gC);
+  TORCH_CHECK(g.sizes() == y.sizes() && norms.numel() == y.size(0), "rownorm_gather_bwd shapes");
+  auto dx = torch::empty_like(g);
+  check_hip(launch_rownorm_bwd(g.data_ptr<float>(), y.data_ptr<float>(), norms.contiguous().data_ptr<float>(),
+                               (int)g.size(0), (int)g.size(1), (float)eps, dx.data_ptr<float>(), cur_stream()),
+            "rownorm_bwd");
+  return dx;
+}
+
 }  // namespace
 
 int small_comm_world(int64_t h) { return h == 0 ? 1 : get(h)->world; }
@@ -377,6 +487,13 @@ void register_comm(pybind11::module& m) {
   m.def("small_comm_world", &small_comm_world);
   m.def("small_comm_ops", &small_comm_ops, "collectives issued on a handle so far");
   m.def("small_all_reduce_", &small_all_reduce_py, "in-place SUM on the current stream");
+  m.def("small_comm_kind", &small_comm_kind, "0 none, 1 RCCL, 2 xGMI, 3 emulated");
+  m.def("small_comm_rank", &small_comm_rank, "this process's rank on the communicator");
+  m.def("small_all_gather", &small_all_gather, "rank-major all-gather along dim 0 (RCCL / emulated)");
+  m.def("small_reduce_scatter", &small_reduce_scatter, "SUM reduce-scatter along dim 0 (RCCL / emulated)");
+  m.def("rownorm_gather", &rownorm_gather,
+        "row L2-normalise into this rank's block of the contrast matrix + in-place all-gather -> (C, norms)");
+  m.def("rownorm_gather_bwd", &rownorm_gather_bwd, "reduce-scatter of dC + row-normalisation gradient");
   m.def("small_comm_stall_", &small_comm_stall_,
         "watchdog drill: bounded GPU stall, then a collective whose completion event waits behind it");
 }

@@ -62,7 +62,7 @@ def _sources():
 
 
 def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False,
-          checked: bool = False) -> str:
+          checked: bool = False, variant: str = "", defines: list | None = None) -> str:
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc_torch, lib_torch, abi = _torch_paths()
     hipcc = _hipcc()
@@ -70,10 +70,13 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = ["-std=c++17", "-fPIC", f"-I{os.path.join(CSRC, 'include')}", "-Wno-unused-result",
               "-Wno-deprecated-declarations"]
-    name = "_C_checked" if checked else "_C"
+    # variant: an experiment build _C_<variant>.so with extra kernel defines (loaded with
+    # SDX_EXT_VARIANT=<variant>), e.g. --variant fragpin --define SDX_FRAG_PIN=1
+    name = "_C_checked" if checked else ("_C_" + variant if variant else "_C")
     out_so = os.path.join(PKG, name + ".so")
     kflags = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-              "-ffp-contract=fast"] + opt + common + (["-DSDX_CHECKED=1"] if checked else [])
+              "-ffp-contract=fast"] + opt + common + (["-DSDX_CHECKED=1"] if checked else []) + \
+        [f"-D{d}" for d in (defines or [])]
     bflags = [os.environ.get("CXX", "g++"), "-O2", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               "-I/opt/rocm/include",
               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
@@ -124,9 +127,12 @@ def main():
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--checked", action="store_true", help="device bounds checks -> _C_checked.so")
     ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--variant", default="", help="experiment build _C_<variant>.so (SDX_EXT_VARIANT)")
+    ap.add_argument("--define", action="append", default=[], help="extra kernel define NAME=VALUE")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
-    out = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose, checked=a.checked)
+    out = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose, checked=a.checked, variant=a.variant,
+                defines=a.define)
     print(out)
 
 

@@ -101,6 +101,8 @@ class PretrainEngine:
             else:
                 self.sync_group = dist.group.WORLD
                 self._setup_syncbn_comm(opt, dev)
+        if world > 1 and self.backend == "native":
+            self._setup_gather_comm(opt, dev)
         model = model.to(dev)
         if dev.type == "cuda":
             model = model.to(memory_format=torch.channels_last)
@@ -169,6 +171,21 @@ class PretrainEngine:
                 logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
             else:
                 logging.warning("SyncBN statistics use the process-group all-reduce")
+
+    def _setup_gather_comm(self, opt, dev):
+        """Native transport of the contrastive loss's embedding all-gather / reduce-scatter
+        (SURVEY §2.3 X5): the dedicated RCCL communicator (the SyncBN one when it is RCCL,
+        else a new one; created and self-checked by all ranks together, 0 everywhere on
+        failure -> c10d). gloo process groups keep the c10d path."""
+        if dev.type != "cuda" or comm.backend() != "nccl" or os.environ.get("SDX_NATIVE_GATHER", "1") == "0":
+            return
+        m = _ext.require()
+        h = comm.native_small_comm(None)
+        if not (h and m.small_comm_kind(h) == 1):
+            h = comm.create_rccl_small_comm(None, float(getattr(opt, "comm_timeout", 600.0)))
+        if h:
+            comm.set_native_gather_comm(None, h)
+            logging.info("contrastive-loss embedding gather: dedicated RCCL communicator (native)")
 
     def _resume(self, path):
         st = ckpt_mod.load_checkpoint(path)

@@ -198,13 +198,28 @@ class DistributedContrastiveLoss(nn.Module):
         w, r = comm.world_size(), comm.rank()
         nv = self.n_views
         b_local = feats.shape[0] // nv
-        n = row_normalize(feats.to(torch.promote_types(feats.dtype, torch.float32)), self.backend)
-        C = comm.all_gather_with_grad(n)
+        x = feats.to(torch.promote_types(feats.dtype, torch.float32))
+        h = comm.native_gather_comm() if (w > 1 and self.backend != "torch" and x.is_cuda) else 0
+        if h and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] <= 256:
+            # normalised rows land in this rank's block of C, gathered in place on the
+            # native RCCL communicator (backward: reduce-scatter) — no c10d call
+            from ..ops.contrastive import row_normalize_gather
+            C = row_normalize_gather(x, h)
+            n = C[r * x.shape[0]:(r + 1) * x.shape[0]]
+        else:
+            h = 0
+            n = row_normalize(x, self.backend)
+            C = comm.all_gather_with_grad(n)
         labels_all = None
         if self.method == "SupCon":
             if labels is None:
                 raise ValueError("SupCon needs labels")
-            labels_all = comm.all_gather_tensor(labels.to(torch.int64).contiguous())
+            lab = labels.to(torch.int64).contiguous()
+            if h:
+                from ..ops import _ext
+                labels_all = _ext.require().small_all_gather(h, lab)
+            else:
+                labels_all = comm.all_gather_tensor(lab)
         self_idx, akey, ckey = self._indices(b_local, w, r, feats.device, labels_all)
         A = n if self.contrast_mode == "all" else n[:b_local]
         n_anchor_global = A.shape[0] * w

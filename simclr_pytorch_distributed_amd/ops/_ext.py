@@ -51,7 +51,9 @@ def ext():
                 finally:
                     sys.path.pop(0)
             # SDX_CHECKED=1: the bounds-checked build (csrc/build.py --checked)
-            name = "_C_checked" if os.environ.get("SDX_CHECKED", "0") == "1" else "_C"
+            # SDX_EXT_VARIANT=v: an experiment build (csrc/build.py --variant v)
+            var = os.environ.get("SDX_EXT_VARIANT", "")
+            name = "_C_checked" if os.environ.get("SDX_CHECKED", "0") == "1" else ("_C_" + var if var else "_C")
             _mod = importlib.import_module("simclr_pytorch_distributed_amd." + name)
         except Exception as e:  # noqa: BLE001
             _err = e

@@ -62,6 +62,33 @@ class _RowNorm(torch.autograd.Function):
         return _ext.require().rownorm_bwd(dy.contiguous(), y, norms, ctx.eps), None
 
 
+class _RowNormGather(torch.autograd.Function):
+    """Row L2 normalisation written straight into this rank's block of the gathered
+    contrast matrix, all-gathered in place on a native communicator (RCCL; an emulated
+    one in single-GPU tests); backward: reduce-scatter of dC to the row owners, then the
+    normalisation gradient (csrc/bindings/comm_ops.cpp rownorm_gather[_bwd])."""
+
+    @staticmethod
+    def forward(ctx, x, handle, eps):
+        C, norms = _ext.require().rownorm_gather(handle, x.contiguous(), eps)
+        ctx.save_for_backward(C, norms)
+        ctx.meta = (handle, eps, x.shape[0])
+        return C
+
+    @staticmethod
+    def backward(ctx, gC):
+        C, norms = ctx.saved_tensors
+        handle, eps, n = ctx.meta
+        m = _ext.require()
+        r = m.small_comm_rank(handle)
+        return m.rownorm_gather_bwd(handle, gC.contiguous(), C[r * n:(r + 1) * n], norms, eps), None, None
+
+
+def row_normalize_gather(x: torch.Tensor, handle: int, eps: float = 1e-12) -> torch.Tensor:
+    """``all_gather(F.normalize(x, dim=1))`` (rank-major) with reduce-scatter backward."""
+    return _RowNormGather.apply(x, handle, eps)
+
+
 def row_normalize(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
     """Row L2 normalisation (reference main_supcon.py:283, ``F.normalize(dim=1)``)."""
     if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.shape[1] <= 256 and _ext.available():

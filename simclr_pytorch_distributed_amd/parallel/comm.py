@@ -162,6 +162,23 @@ def native_small_comm(group) -> int:
     return _native.get(_key(group), 0)
 
 
+_gather = {}
+
+
+def set_native_gather_comm(group, handle: int) -> None:
+    """Register a native RCCL (or emulated) communicator that carries the contrastive
+    loss's embedding all-gather / reduce-scatter for ``group`` (SURVEY §2.3 X5);
+    ``handle=0`` unregisters (c10d path)."""
+    if handle:
+        _gather[_key(group)] = int(handle)
+    else:
+        _gather.pop(_key(group), None)
+
+
+def native_gather_comm(group=None) -> int:
+    return _gather.get(_key(group), 0)
+
+
 def _agree_device(group=None) -> torch.device:
     if dist.get_backend(group) == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
@@ -238,6 +255,14 @@ def create_rccl_small_comm(group=None, timeout_s: float = 600.0) -> int:
         m.small_all_reduce_(st["h"], probe)
         if float(probe[0].item()) != float(w):
             raise RuntimeError(f"RCCL small communicator self-check failed ({probe[0].item()} != {w})")
+        # rank-major all-gather + reduce-scatter (the contrastive loss's embedding exchange)
+        g = m.small_all_gather(st["h"], torch.full((2, 8), float(r), device=dev))
+        want = torch.arange(w, device=dev, dtype=torch.float32).repeat_interleave(2)[:, None].expand(-1, 8)
+        if not torch.equal(g, want):
+            raise RuntimeError("RCCL small communicator all-gather self-check failed")
+        rs = m.small_reduce_scatter(st["h"], torch.ones(2 * w, 8, device=dev))
+        if not torch.equal(rs, torch.full((2, 8), float(w), device=dev)):
+            raise RuntimeError("RCCL small communicator reduce-scatter self-check failed")
 
     def cleanup():
         if st["h"]:

@@ -98,3 +98,35 @@ def test_native_executor_syncbn_path(gpu, name, which):
         g0, g1 = getattr(b0, n).bias.grad, getattr(b1, n).bias.grad
         assert torch.allclose(g0, g1, rtol=1e-3, atol=1e-5), n
     m.small_comm_destroy(h)
+
+
+@pytest.mark.parametrize("kind", ["rccl1", "emu3"])
+def test_native_gather_scatter(gpu, kind):
+    """Embedding exchange of the contrastive loss on a native communicator:
+    rank-major all-gather, SUM reduce-scatter, and the fused normalise-into-C + in-place
+    gather with its autograd backward, vs plain torch (1-rank RCCL: the real ncclAllGather /
+    ncclReduceScatter calls; emulated W=3: identical virtual ranks)."""
+    import torch.nn.functional as F
+    from simclr_pytorch_distributed_amd.ops.contrastive import row_normalize_gather
+    m = _m()
+    h = m.rccl_comm_init(m.rccl_unique_id(), 1, 0) if kind == "rccl1" else m.emu_small_comm(3)
+    W = m.small_comm_world(h)
+    try:
+        x = torch.randn(37, 128, device=gpu)
+        g = m.small_all_gather(h, x)
+        assert torch.equal(g, x.repeat(W, 1))
+        lab = torch.randint(0, 10, (37,), device=gpu)
+        assert torch.equal(m.small_all_gather(h, lab), lab.repeat(W))
+        gc = torch.randn(W * 37, 128, device=gpu)
+        assert torch.allclose(m.small_reduce_scatter(h, gc), W * gc[:37])
+        xa = x.clone().requires_grad_(True)
+        C = row_normalize_gather(xa, h)
+        ref = F.normalize(x.double(), dim=1)
+        assert torch.allclose(C.double(), ref.repeat(W, 1), rtol=1e-6, atol=1e-6)
+        C.backward(gc)
+        xr = x.double().clone().requires_grad_(True)
+        F.normalize(xr, dim=1).backward(W * gc[:37].double())   # identical ranks: W x own block
+        assert torch.allclose(xa.grad.double(), xr.grad, rtol=1e-4, atol=1e-5)
+        assert m.small_comm_kind(h) == (1 if kind == "rccl1" else 3) and m.small_comm_rank(h) == 0
+    finally:
+        m.small_comm_destroy(h)
