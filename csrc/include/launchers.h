@@ -134,7 +134,8 @@ hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, in
                               uint64_t seed, const float* mean, const float* std, float scale_lo, float scale_hi,
                               float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
                               float sat, float hue, float gray_p, int do_crop, int do_flip, const int64_t* seed_dev,
-                              void* out, hipStream_t s, long n_data = 0);
+                              void* out, hipStream_t s, long n_data = 0, const int64_t* offs = nullptr,
+                              const int32_t* hw = nullptr);
 
 // ---- optimizers (optim.hip) -----------------------------------------------------
 hipError_t launch_sgd(float* p, const float* g, float* buf, long n, const float* lr, float momentum, float wd,

@@ -35,7 +35,9 @@ struct Rng {
 };
 
 struct AugParams {
-  const uint8_t* data;     // [n_data][H][W][3]
+  const uint8_t* data;     // [n_data][H][W][3], or ragged (offs != nullptr): image i at data + offs[i]
+  const int64_t* offs;     // optional [n_data] byte offsets of native-resolution images
+  const int32_t* hw;       // optional [n_data][2] their (height, width)
   long n_data;             // images in `data` (bounds checks)
   const int64_t* idx;      // [B]
   uint16_t* out;           // [n_views*B][S][S][8]
@@ -55,8 +57,8 @@ struct ViewParams {
   int order[4];            // 0 brightness, 1 contrast, 2 saturation, 3 hue
 };
 
-__device__ void make_view_params(const AugParams& p, Rng& rng, ViewParams& v) {
-  const float H = p.H, W = p.W;
+__device__ void make_view_params(const AugParams& p, Rng& rng, ViewParams& v, int Hi, int Wi) {
+  const float H = Hi, W = Wi;
   v.ci = 0.f; v.cj = 0.f; v.ch = H; v.cw = W;
   if (p.do_crop) {
     const float area = H * W;
@@ -131,21 +133,21 @@ __device__ void adjust_hue(float& r, float& g, float& b, float hf) {
 }
 
 // bilinear sample (align_corners=False) of the crop box, then flip
-__device__ void sample_pixel(const AugParams& p, const uint8_t* img, const ViewParams& v, int oy, int ox,
-                             float& r, float& g, float& b) {
+__device__ void sample_pixel(const AugParams& p, const uint8_t* img, int H, int W, const ViewParams& v, int oy,
+                             int ox, float& r, float& g, float& b) {
   const int xs = v.flip ? (p.S - 1 - ox) : ox;
   float sy = (oy + 0.5f) * (v.ch / p.S) - 0.5f + v.ci;
   float sx = (xs + 0.5f) * (v.cw / p.S) - 0.5f + v.cj;
   sy = fminf(fmaxf(sy, v.ci), v.ci + v.ch - 1.f);
   sx = fminf(fmaxf(sx, v.cj), v.cj + v.cw - 1.f);
   const int y0 = (int)floorf(sy), x0 = (int)floorf(sx);
-  const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
+  const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
   const float wy = sy - y0, wx = sx - x0;
-  SDX_DCHECK(y0 >= 0 && x0 >= 0 && y0 < p.H && x0 < p.W && y1 < p.H && x1 < p.W);
-  const uint8_t* p00 = img + ((size_t)y0 * p.W + x0) * 3;
-  const uint8_t* p01 = img + ((size_t)y0 * p.W + x1) * 3;
-  const uint8_t* p10 = img + ((size_t)y1 * p.W + x0) * 3;
-  const uint8_t* p11 = img + ((size_t)y1 * p.W + x1) * 3;
+  SDX_DCHECK(y0 >= 0 && x0 >= 0 && y0 < H && x0 < W && y1 < H && x1 < W);
+  const uint8_t* p00 = img + ((size_t)y0 * W + x0) * 3;
+  const uint8_t* p01 = img + ((size_t)y0 * W + x1) * 3;
+  const uint8_t* p10 = img + ((size_t)y1 * W + x0) * 3;
+  const uint8_t* p11 = img + ((size_t)y1 * W + x1) * 3;
   float c[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -184,11 +186,14 @@ __global__ __launch_bounds__(256) void aug_kernel(AugParams p) {
   const int b = blockIdx.x, view = blockIdx.y;
   const int64_t src = p.idx[b];
   SDX_DCHECK(p.n_data <= 0 || (src >= 0 && src < p.n_data));
-  const uint8_t* img = p.data + (size_t)src * p.H * p.W * 3;
+  // dense [N][H][W][3] store, or native-resolution images (ImageFolder: RandomResizedCrop
+  // samples its box from the original pixels, as torchvision does on the decoded image)
+  const int H = p.offs ? p.hw[2 * src] : p.H, W = p.offs ? p.hw[2 * src + 1] : p.W;
+  const uint8_t* img = p.offs ? p.data + p.offs[src] : p.data + (size_t)src * p.H * p.W * 3;
   if (threadIdx.x == 0) {
     const uint64_t seed = p.seed_dev ? (uint64_t)p.seed_dev[0] : p.seed;
     Rng rng{mix64(seed * 0x100000001b3ull + (uint64_t)src * 31ull + (uint64_t)view * 0x9E37ull + (uint64_t)b), 0};
-    make_view_params(p, rng, vp);
+    make_view_params(p, rng, vp, H, W);
   }
   __syncthreads();
   const ViewParams v = vp;
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(256) void aug_kernel(AugParams p) {
     float acc = 0.f;
     for (int pix = threadIdx.x; pix < npix; pix += 256) {
       float r, g, bb;
-      sample_pixel(p, img, v, pix / p.S, pix % p.S, r, g, bb);
+      sample_pixel(p, img, H, W, v, pix / p.S, pix % p.S, r, g, bb);
       jitter_ops(v, cpos, 0.f, r, g, bb);
       acc += grey(r, g, bb);
     }
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(256) void aug_kernel(AugParams p) {
   uint16_t* out = p.out + ((size_t)view * p.B + b) * npix * 8;
   for (int pix = threadIdx.x; pix < npix; pix += 256) {
     float r, g, bb;
-    sample_pixel(p, img, v, pix / p.S, pix % p.S, r, g, bb);
+    sample_pixel(p, img, H, W, v, pix / p.S, pix % p.S, r, g, bb);
     if (v.jitter) jitter_ops(v, 4, cmean, r, g, bb);
     if (v.gray) { const float gy = grey(r, g, bb); r = g = bb = gy; }
     r = (r - p.mean[0]) * p.inv_std[0];
@@ -231,8 +236,10 @@ hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, in
                               uint64_t seed, const float* mean, const float* std, float scale_lo, float scale_hi,
                               float ratio_lo, float ratio_hi, float jitter_p, float bright, float contrast,
                               float sat, float hue, float gray_p, int do_crop, int do_flip, const int64_t* seed_dev,
-                              void* out, hipStream_t s, long n_data) {
+                              void* out, hipStream_t s, long n_data, const int64_t* offs, const int32_t* hw) {
   AugParams p{};
+  p.offs = offs;
+  p.hw = hw;
   p.n_data = n_data;
   p.data = data; p.idx = idx; p.out = (uint16_t*)out;
   p.B = B; p.H = H; p.W = W; p.S = S; p.n_views = n_views; p.seed = seed;

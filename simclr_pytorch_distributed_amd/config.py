@@ -10,7 +10,9 @@ Additions (new flags only; no reference flag changes meaning):
 ``--precision``, ``--backend``, ``--synthetic``, ``--stem``, ``--optimizer {sgd,lars}``,
 ``--grad_semantics {ref,exact}`` (Q2), ``--dist_backend``, ``--seed``, ``--head``,
 ``--feat_dim`` (Q11), ``--resume``, ``--cuda_graph``, ``--work_dir``.
-Fixes: ``--num_workers`` is honoured (Q6); ``dataset=path`` parses ``--mean/--std``
+Fixes: ``--num_workers`` is honoured (Q6): it sizes the image-decode thread pool of
+``dataset=path`` and the CPU augmentation threads of ``--gpu_aug 0`` (the default pipeline
+is the GPU kernel, which needs no workers); ``dataset=path`` parses ``--mean/--std``
 safely and uses the std (Q5); run folders get a collision guard (Q21).
 """
 from __future__ import annotations
@@ -67,7 +69,8 @@ def _add_common_new_flags(p: argparse.ArgumentParser):
     g.add_argument("--dist_backend", type=str, default="auto", choices=["auto", "nccl", "gloo"])
     g.add_argument("--cuda_graph", action="store_true", help="capture the train step in a HIP graph")
     g.add_argument("--max_steps", type=int, default=0, help="stop each epoch after this many steps (0 = all)")
-    g.add_argument("--gpu_aug", type=int, default=1, help="run augmentation on the GPU (1) or CPU (0)")
+    g.add_argument("--gpu_aug", type=int, default=1,
+                   help="augmentation on the GPU kernel (1) or the CPU torch pipeline on --num_workers threads (0)")
     g.add_argument("--syncbn_comm", type=str, default="rccl", choices=["rccl", "xgmi"],
                    help="SyncBN statistic all-reduce: RCCL, or the one-shot xGMI peer-memory kernel")
     g.add_argument("--comm_timeout", type=float, default=600.0,

@@ -73,13 +73,16 @@ class AugConfig:
                          gray_p=0.0, crop=False, flip=False, mean=mean, std=std)
 
 
-def gpu_augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed, seed_t=None) -> torch.Tensor:
-    """``seed_t``: optional int64 device scalar read by the kernel at run time (graph replays)."""
+def gpu_augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed, seed_t=None, offs=None,
+                hw=None) -> torch.Tensor:
+    """``seed_t``: optional int64 device scalar read by the kernel at run time (graph replays).
+    ``offs``/``hw``: a ragged native-resolution store (``data`` flat uint8, int64 byte
+    offsets, int32 [N, 2] sizes; data/datasets.py load_image_folder)."""
     m = _ext.require()
     return m.gpu_augment(data, idx, cfg.size, cfg.n_views, int(seed) & ((1 << 63) - 1), list(cfg.mean),
                          list(cfg.std), cfg.scale[0], cfg.scale[1], cfg.ratio[0], cfg.ratio[1], cfg.jitter_p,
                          cfg.brightness, cfg.contrast, cfg.saturation, cfg.hue, cfg.gray_p, cfg.crop, cfg.flip,
-                         seed_t)
+                         seed_t, offs, hw)
 
 
 def _view_params(cfg: AugConfig, H: int, W: int, rng: _Rng):
@@ -158,12 +161,14 @@ def _hue(img, hf):
     return torch.stack([rr.gather(0, sel)[0], gg.gather(0, sel)[0], bb.gather(0, sel)[0]])
 
 
-def augment_reference(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed: int) -> torch.Tensor:
+def augment_reference(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed: int, offs=None,
+                      hw=None) -> torch.Tensor:
     """CPU torch implementation with identical draws; returns NHWC float [V*B, S, S, 8]."""
     data = data.cpu()
     idx = idx.cpu()
+    if offs is not None:
+        offs, hw = offs.cpu(), hw.cpu()
     B = idx.shape[0]
-    H, W = data.shape[1], data.shape[2]
     S = cfg.size
     seed = int(seed) & ((1 << 63) - 1)
     out = torch.zeros(cfg.n_views * B, S, S, 8)
@@ -172,9 +177,15 @@ def augment_reference(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, see
     for v in range(cfg.n_views):
         for b in range(B):
             src = int(idx[b])
+            if offs is None:
+                H, W = data.shape[1], data.shape[2]
+                img = data[src].float()   # H W 3
+            else:
+                H, W = int(hw[src, 0]), int(hw[src, 1])
+                o = int(offs[src])
+                img = data[o:o + H * W * 3].view(H, W, 3).float()
             key = _mix64((seed * 0x100000001B3 + src * 31 + v * 0x9E37 + b) & M64)
             p = _view_params(cfg, H, W, _Rng(key))
-            img = data[src].float()   # H W 3
             xs = (S - 1 - ox) if p["flip"] else ox
             sy = ((oy + 0.5) * (p["ch"] / S) - 0.5 + p["ci"]).clamp(p["ci"], p["ci"] + p["ch"] - 1)
             sx = ((xs + 0.5) * (p["cw"] / S) - 0.5 + p["cj"]).clamp(p["cj"], p["cj"] + p["cw"] - 1)
@@ -205,11 +216,11 @@ def augment_reference(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, see
     return out
 
 
-def augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed: int) -> torch.Tensor:
+def augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed: int, offs=None, hw=None) -> torch.Tensor:
     """Dispatch: GPU kernel for GPU tensors, torch reference otherwise (NHWC, C=8)."""
     if data.is_cuda:
-        return gpu_augment(data, idx, cfg, seed)
-    return augment_reference(data, idx, cfg, seed)
+        return gpu_augment(data, idx, cfg, seed, offs=offs, hw=hw)
+    return augment_reference(data, idx, cfg, seed, offs, hw)
 
 
 def nhwc8_to_nchw(x: torch.Tensor) -> torch.Tensor:

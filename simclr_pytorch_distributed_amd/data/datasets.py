@@ -21,13 +21,29 @@ import numpy as np
 
 @dataclass
 class ArrayDataset:
-    images: np.ndarray      # uint8 [N, H, W, 3]
+    images: np.ndarray      # uint8 [N, H, W, 3], or a flat uint8 byte store (ragged)
     labels: np.ndarray      # int64 [N]
     num_classes: int
     name: str = ""
+    # ragged store of native-resolution images: image i is images[offsets[i]:][:h*w*3]
+    # with (h, w) = sizes[i] (int64 [N] / int32 [N, 2]); None for a dense store
+    offsets: Optional[np.ndarray] = None
+    sizes: Optional[np.ndarray] = None
 
     def __len__(self):
-        return int(self.images.shape[0])
+        return int(self.labels.shape[0])
+
+    @property
+    def ragged(self) -> bool:
+        return self.offsets is not None
+
+    def image(self, i: int) -> np.ndarray:
+        """Image i as uint8 [h, w, 3] (either store)."""
+        if not self.ragged:
+            return self.images[i]
+        h, w = (int(v) for v in self.sizes[i])
+        o = int(self.offsets[i])
+        return self.images[o:o + h * w * 3].reshape(h, w, 3)
 
 
 _CIFAR = {
@@ -104,33 +120,56 @@ def synthetic_dataset(n: int = 50000, size: int = 32, num_classes: int = 10, see
     return ArrayDataset(imgs, labels, num_classes, "synthetic")
 
 
-def load_image_folder(root: str, size: Optional[int] = None) -> ArrayDataset:
-    """ImageFolder (class-per-subdirectory) decoded with PIL into a uint8 array.
+def load_image_folder(root: str, size: Optional[int] = None, workers: int = 1) -> ArrayDataset:
+    """ImageFolder (class-per-subdirectory) decoded with PIL into uint8 RGB.
 
-    Images are resized to ``size`` x ``size`` (if given) so the dataset can be stored as
-    one dense array for the GPU augmentation kernel.
+    ``size=None`` (pretraining): every image is kept at its NATIVE resolution in a ragged
+    byte store (offsets + sizes), so the GPU RandomResizedCrop samples its box from the
+    original pixels exactly as torchvision does on the decoded image (main_supcon.py:170-
+    191); ``size=s``: resized to s x s into a dense [N, s, s, 3] array. Decoding runs on
+    ``workers`` threads (``--num_workers``; PIL releases the GIL while decoding).
     """
+    from concurrent.futures import ThreadPoolExecutor
+
     from PIL import Image
     classes = sorted(d for d in os.listdir(root) if os.path.isdir(os.path.join(root, d)))
     exts = (".jpg", ".jpeg", ".png", ".ppm", ".bmp", ".pgm", ".tif", ".tiff", ".webp")
-    xs, ys = [], []
+    files, ys = [], []
     for ci, cname in enumerate(classes):
         cdir = os.path.join(root, cname)
-        for dp, _, files in sorted(os.walk(cdir)):
-            for f in sorted(files):
+        for dp, _, fs in sorted(os.walk(cdir)):
+            for f in sorted(fs):
                 if f.lower().endswith(exts):
-                    im = Image.open(os.path.join(dp, f)).convert("RGB")
-                    if size is not None:
-                        im = im.resize((size, size), Image.BILINEAR)
-                    xs.append(np.asarray(im, dtype=np.uint8))
+                    files.append(os.path.join(dp, f))
                     ys.append(ci)
-    if not xs:
+    if not files:
         raise FileNotFoundError(f"no images under {root!r}")
-    return ArrayDataset(np.stack(xs), np.asarray(ys, dtype=np.int64), len(classes), os.path.basename(root))
+
+    def decode(path):
+        with Image.open(path) as im:
+            im = im.convert("RGB")
+            if size is not None:
+                im = im.resize((size, size), Image.BILINEAR)
+            return np.asarray(im, dtype=np.uint8)
+
+    with ThreadPoolExecutor(max_workers=max(1, int(workers))) as ex:
+        xs = list(ex.map(decode, files))
+    labels = np.asarray(ys, dtype=np.int64)
+    name = os.path.basename(os.path.normpath(root))
+    if size is not None:
+        return ArrayDataset(np.stack(xs), labels, len(classes), name)
+    sizes = np.asarray([x.shape[:2] for x in xs], dtype=np.int32)
+    nbytes = sizes[:, 0].astype(np.int64) * sizes[:, 1] * 3
+    offsets = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.int64)
+    flat = np.concatenate([x.reshape(-1) for x in xs])
+    return ArrayDataset(flat, labels, len(classes), name, offsets=offsets, sizes=sizes)
 
 
 def build_dataset(dataset: str, data_folder: str, train: bool = True, synthetic: bool = False,
-                  synthetic_size: int = 50000, size: int = 32, seed: int = 0) -> ArrayDataset:
+                  synthetic_size: int = 50000, size: int = 32, seed: int = 0, native: bool = False,
+                  workers: int = 1) -> ArrayDataset:
+    """``native``: an ImageFolder (``dataset='path'``) keeps native resolutions (ragged
+    store) for RandomResizedCrop; otherwise it is resized to ``size``."""
     if synthetic:
         ncls = {"cifar10": 10, "cifar100": 100}.get(dataset, 10)
         n = synthetic_size if train else max(1000, synthetic_size // 5)
@@ -138,5 +177,5 @@ def build_dataset(dataset: str, data_folder: str, train: bool = True, synthetic:
     if dataset in _CIFAR:
         return load_cifar(dataset, data_folder, train)
     if dataset == "path":
-        return load_image_folder(data_folder, size)
+        return load_image_folder(data_folder, None if native else size, workers)
     raise ValueError(f"dataset not supported: {dataset}")

@@ -62,8 +62,11 @@ class LinearEngine:
         self.criterion = torch.nn.CrossEntropyLoss()
         self.optimizer = torch.optim.SGD(self.classifier.parameters(), lr=opt.learning_rate, momentum=opt.momentum,
                                          weight_decay=opt.weight_decay)
-        tr = build_dataset(opt.dataset, opt.data_folder, True, opt.synthetic, opt.synthetic_size, 32, opt.seed)
-        va = build_dataset(opt.dataset, opt.data_folder, False, opt.synthetic, opt.synthetic_size, 32, opt.seed)
+        nw = getattr(opt, "num_workers", 1)
+        tr = build_dataset(opt.dataset, opt.data_folder, True, opt.synthetic, opt.synthetic_size, 32, opt.seed,
+                           workers=nw)
+        va = build_dataset(opt.dataset, opt.data_folder, False, opt.synthetic, opt.synthetic_size, 32, opt.seed,
+                           workers=nw)
         self.tr_x, self.tr_y = torch.from_numpy(tr.images).to(dev), torch.from_numpy(tr.labels).to(dev)
         self.va_x, self.va_y = torch.from_numpy(va.images).to(dev), torch.from_numpy(va.labels).to(dev)
         # the reference DataLoader keeps the last partial batch (main_ce.py set_loader)

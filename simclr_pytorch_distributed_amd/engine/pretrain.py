@@ -116,8 +116,12 @@ class PretrainEngine:
         self.criterion = DistributedContrastiveLoss(opt.method, opt.temp, opt.base_temperature, opt.contrast_mode,
                                                     backend="native" if self.backend == "native" else "torch")
         # data: whole uint8 dataset resident on the device
-        ds = build_dataset(opt.dataset, opt.data_folder, True, opt.synthetic, opt.synthetic_size, opt.size, opt.seed)
+        ds = build_dataset(opt.dataset, opt.data_folder, True, opt.synthetic, opt.synthetic_size, opt.size, opt.seed,
+                           native=True, workers=opt.num_workers)
         self.data = torch.from_numpy(ds.images).to(dev)
+        # ImageFolder: native-resolution ragged store (RandomResizedCrop on original pixels)
+        self.data_offs = torch.from_numpy(ds.offsets).to(dev) if ds.ragged else None
+        self.data_hw = torch.from_numpy(ds.sizes).to(dev) if ds.ragged else None
         self.labels = torch.from_numpy(ds.labels).to(dev)
         self.sampler = DistributedIndexSampler(len(ds), opt.local_batch, world, rank, seed=opt.seed)
         self.aug = AugConfig.simclr(opt.size, opt.mean_t, opt.std_t)
@@ -207,13 +211,30 @@ class PretrainEngine:
 
     # ------------------------------------------------------------------------------
     def make_views(self, idx: torch.Tensor, epoch: int = 1, it: int = 0) -> torch.Tensor:
+        if not getattr(self.opt, "gpu_aug", 1):
+            return self._make_views_cpu(idx, epoch, it)
         if self.backend == "native":
             # the seed is read from device memory by the kernel (graph-replay safe)
-            x = augment_gpu(self.data, idx, self.aug, 0, self._seed_t)
+            x = augment_gpu(self.data, idx, self.aug, 0, self._seed_t, self.data_offs, self.data_hw)
         else:
-            x = augment(self.data, idx, self.aug, step_seed(self.opt.seed, epoch, it, self.rank))
+            x = augment(self.data, idx, self.aug, step_seed(self.opt.seed, epoch, it, self.rank), self.data_offs,
+                        self.data_hw)
             x = nhwc8_to_nchw(x)
         return x
+
+    def _make_views_cpu(self, idx, epoch, it):
+        """``--gpu_aug 0``: the torch CPU pipeline (same draws as the kernel) on a host copy
+        of the dataset, ``--num_workers`` intra-op threads, then moved to the device."""
+        if getattr(self, "_cpu_data", None) is None:
+            torch.set_num_threads(max(1, int(self.opt.num_workers)))
+            self._cpu_data = self.data.cpu()
+            self._cpu_offs = self.data_offs.cpu() if self.data_offs is not None else None
+            self._cpu_hw = self.data_hw.cpu() if self.data_hw is not None else None
+        x = augment(self._cpu_data, idx.cpu(), self.aug, step_seed(self.opt.seed, epoch, it, self.rank),
+                    self._cpu_offs, self._cpu_hw)
+        if self.backend == "native":
+            return x.to(self.device, torch.bfloat16)
+        return nhwc8_to_nchw(x).to(self.device)
 
     def _host_prelude(self, epoch: int, it: int, iters: int):
         """Per-step host-side scalars, written to device tensors the step body reads."""

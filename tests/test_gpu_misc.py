@@ -23,6 +23,25 @@ def test_gpu_augment_matches_reference(gpu):
         assert torch.all(out[..., 3:] == 0)
 
 
+def test_gpu_augment_ragged_native_resolution(gpu):
+    """ImageFolder store at native resolutions (ragged: flat bytes + offsets + sizes): the
+    kernel crops from each image's own pixels, same draws as the torch reference."""
+    from simclr_pytorch_distributed_amd.data.augment import AugConfig, augment_reference, gpu_augment
+    g = torch.Generator().manual_seed(1)
+    shapes = [(48, 64), (100, 75), (33, 33), (64, 128), (90, 40), (57, 71)]
+    imgs = [torch.randint(0, 256, (h, w, 3), generator=g, dtype=torch.uint8) for h, w in shapes]
+    flat = torch.cat([i.reshape(-1) for i in imgs])
+    hw = torch.tensor(shapes, dtype=torch.int32)
+    offs = torch.cumsum(torch.tensor([0] + [h * w * 3 for h, w in shapes[:-1]]), 0).to(torch.int64)
+    idx = torch.tensor([5, 0, 3, 1, 4, 2, 3, 1])
+    for cfg in (AugConfig.simclr(32, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25)),
+                AugConfig.evaluation(24, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25))):
+        out = gpu_augment(flat.to(gpu), idx.to(gpu), cfg, 9, offs=offs.to(gpu), hw=hw.to(gpu)).float().cpu()
+        ref = augment_reference(flat, idx, cfg, 9, offs, hw)
+        err = (out - ref).abs().amax(dim=(1, 2, 3))
+        assert (err < 0.05).float().mean() >= 0.85, err
+
+
 @pytest.mark.parametrize("kind", ["sgd", "lars"])
 def test_fused_optimizer_kernels(gpu, kind):
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams, FusedLARS, FusedSGD

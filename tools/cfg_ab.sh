@@ -1,3 +1,7 @@
+#!/bin/bash
+# conv tile-config A/B on the GPU box: tools/conv_bench.py totals for the auto choice, the
+# 256x128 8-wave tile, and the 3-buffer LDS-DMA ring (SDX_IGEMM_RING=1) on cfg 0/4/5.
+# Result: profiles/conv_cfg_ring_ab_r2.txt
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
