@@ -62,7 +62,7 @@ def _sources():
 
 
 def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False,
-          checked: bool = False, variant: str = "", defines: list | None = None) -> str:
+          checked: bool = False, variant: str = "", defines: list | None = None, sanitize: bool = False) -> str:
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc_torch, lib_torch, abi = _torch_paths()
     hipcc = _hipcc()
@@ -72,6 +72,12 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
               "-Wno-deprecated-declarations"]
     # variant: an experiment build _C_<variant>.so with extra kernel defines (loaded with
     # SDX_EXT_VARIANT=<variant>), e.g. --variant fragpin --define SDX_FRAG_PIN=1
+    # sanitize: _C_san.so, the host binding layer (csrc/bindings) built with AddressSanitizer
+    # + UndefinedBehaviorSanitizer (GCC runtimes); the device kernels are unchanged (GPU ASan
+    # is not available). Load it under the ASan-instrumented Python launcher of
+    # build_asan_python() (the ASan runtime must come first) with SDX_EXT_VARIANT=san.
+    if sanitize:
+        variant = "san"
     name = "_C_checked" if checked else ("_C_" + variant if variant else "_C")
     out_so = os.path.join(PKG, name + ".so")
     kflags = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
@@ -80,7 +86,8 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     bflags = [os.environ.get("CXX", "g++"), "-O2", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               "-I/opt/rocm/include",
               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
-              f"-DTORCH_EXTENSION_NAME={name}", f"-I{py_inc}"] + [f"-I{p}" for p in inc_torch] + common
+              f"-DTORCH_EXTENSION_NAME={name}", f"-I{py_inc}"] + [f"-I{p}" for p in inc_torch] + common + \
+        (SAN_FLAGS if sanitize else [])
     hdr_m = _headers_mtime()
     kern, bind = _sources()
 
@@ -110,6 +117,8 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         for p in lib_torch:
             libs += [f"-L{p}", f"-Wl,-rpath,{p}"]
         libs += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]  # RCCL symbols resolve from torch's own librccl.so (a dependency of libtorch_hip)
+        if sanitize:
+            libs += _gcc_san_libs()
         tmp = out_so + ".tmp"
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + libs
         if verbose:
@@ -121,6 +130,37 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     return out_so
 
 
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-g1"]
+
+
+def _gcc_san_libs():
+    libs = []
+    for n in ("libasan.so", "libubsan.so"):
+        p = subprocess.run(["gcc", f"-print-file-name={n}"], capture_output=True, text=True).stdout.strip()
+        libs += [p, f"-Wl,-rpath,{os.path.dirname(p)}"]
+    return libs
+
+
+ASAN_PY = os.path.join(ROOT, "build", "asan_python")
+
+
+def build_asan_python(force: bool = False) -> str:
+    """A Python interpreter executable linked with the GCC ASan/UBSan runtimes, so the
+    sanitizer runtime is first in the process and ``_C_san.so`` can be imported (the host
+    binding layer runs instrumented; torch and the device kernels are not)."""
+    src = os.path.join(CSRC, "tools", "asan_python.cpp")
+    if not force and os.path.exists(ASAN_PY) and os.path.getmtime(ASAN_PY) >= os.path.getmtime(src):
+        return ASAN_PY
+    os.makedirs(os.path.dirname(ASAN_PY), exist_ok=True)
+    cfg = sysconfig.get_config_vars()
+    cmd = ["g++", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer", f"-I{sysconfig.get_paths()['include']}",
+           src, "-o", ASAN_PY, f"-L{cfg['LIBDIR']}", f"-lpython{cfg['VERSION']}", f"-Wl,-rpath,{cfg['LIBDIR']}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan_python build failed\n{r.stderr}")
+    return ASAN_PY
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
@@ -129,10 +169,14 @@ def main():
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--variant", default="", help="experiment build _C_<variant>.so (SDX_EXT_VARIANT)")
     ap.add_argument("--define", action="append", default=[], help="extra kernel define NAME=VALUE")
+    ap.add_argument("--sanitize", action="store_true",
+                    help="host bindings under ASan+UBSan -> _C_san.so (+ the build/asan_python launcher)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     out = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose, checked=a.checked, variant=a.variant,
-                defines=a.define)
+                defines=a.define, sanitize=a.sanitize)
+    if a.sanitize:
+        print(build_asan_python())
     print(out)
 
 

@@ -284,7 +284,12 @@ class PretrainEngine:
         its slice of the feature gradient. Activation memory is one chunk's; the loss and
         its gradient are those of the full batch. BatchNorm statistics are per chunk (as
         in any micro-batched BN network); running statistics are updated once per chunk
-        in the re-encode pass only. The bucket reducer stays paused until the last chunk.
+        in the re-encode pass only. The update is therefore the EXACT gradient of the
+        full-batch loss of the same network with ghost batch norm of ``mb`` views — not the
+        reference's full-batch BN (tests/test_gradcache.py pins this equivalence); for
+        full-batch BN semantics run the whole local batch in one pass (288 GB of HBM holds
+        the config-5 batch: profiles/cfg5_slice_r2.json). The bucket reducer stays paused
+        until the last chunk.
         """
         opt = self.opt
         ph = self.prof.phase

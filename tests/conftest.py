@@ -19,7 +19,9 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from simclr_pytorch_distributed_amd.ops import _ext
-    _ext.require()  # native path must load on a GPU box (fail loudly, never fall back)
+    m = _ext.require()  # native path must load on a GPU box (fail loudly, never fall back)
+    var = os.environ.get("SDX_EXT_VARIANT", "")
+    assert not var or m.__name__.endswith("_C_" + var), (m.__name__, var)   # e.g. the sanitizer build
     yield torch.device("cuda:0")
     # drop tensors kept alive for side-stream wgrads by tests that ran a backward
     # without an optimizer step / reducer join (ops/streams.py)
