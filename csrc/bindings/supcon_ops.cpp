@@ -62,12 +62,14 @@ std::vector<torch::Tensor> supcon_bwd(torch::Tensor A, torch::Tensor C, torch::T
   TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.numel() == 1, "g must be a GPU float scalar");
   c10::DeviceGuard dg(A.device());
   auto gc = g.contiguous();
-  auto dA = torch::zeros_like(A);
-  auto dC = torch::zeros_like(C);
+  auto dA = torch::empty_like(A);
+  auto dC = torch::empty_like(C);
+  auto ws = torch::empty({std::max<long>(1, supcon_bwd_workspace((int)Na, (int)N, (int)D))}, A.options());
   check_hip(launch_supcon_bwd(A.data_ptr<float>(), C.data_ptr<float>(), a_self.data_ptr<int>(),
                               a_key.data_ptr<int>(), c_key.data_ptr<int>(), lse.data_ptr<float>(),
                               invcnt.data_ptr<float>(), (int)Na, (int)N, (int)D, (float)inv_temp, (float)w,
-                              gc.data_ptr<float>(), dA.data_ptr<float>(), dC.data_ptr<float>(), cur_stream()),
+                              gc.data_ptr<float>(), dA.data_ptr<float>(), dC.data_ptr<float>(),
+                              ws.data_ptr<float>(), cur_stream()),
             "supcon_bwd");
   return {dA, dC};
 }

@@ -22,9 +22,11 @@ hipError_t launch_supcon_fwd(const float* A, const float* C, const int* a_self, 
                              const int* c_key, int Na, int N, int D, float inv_temp, float temp_ratio,
                              float scale, int n_split, float* part, float* lse, float* invcnt,
                              float* row_loss, float* loss, hipStream_t s);
+// ws: fp32 workspace of supcon_bwd_workspace(Na, N, D) elements (per-split partial slabs)
+long supcon_bwd_workspace(int Na, int N, int D);
 hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, const int* a_key,
                              const int* c_key, const float* lse, const float* invcnt, int Na, int N, int D,
-                             float inv_temp, float w, const float* gscale, float* dA, float* dC,
+                             float inv_temp, float w, const float* gscale, float* dA, float* dC, float* ws,
                              hipStream_t s);
 
 // ---- implicit-GEMM convolution (igemm.hip) ------------------------------------

@@ -6,6 +6,9 @@
 // contrast matrix C[N][D]; anchor i has contrast index self[i] and key akey[i];
 // contrast j has key ckey[j]; positive(i,j) <=> akey[i]==ckey[j] && j!=self[i].
 //
+// The backward is deterministic: every split writes its own slice of a partial slab and
+// the slices are summed in split order (no atomics).
+//
 // One kernel template serves three modes. A workgroup (4 waves) owns 64 "own" rows
 // (16 per wave, one own row per lane column of the MFMA tile) and streams the "other"
 // rows through LDS in 32-row tiles (shared by the 4 waves):
@@ -43,7 +46,8 @@ struct SupconParams {
   const float* lse;      // [Na]   (bwd)
   const float* invcnt;   // [Na]   (bwd; <0 marks an anchor without positives)
   float* part;           // fwd: [4][S][n_own]
-  float* out;            // bwd: [n_own][D] (accumulated with atomics)
+  float* out;            // bwd: [n_split][n_own][D] partial slab (one slice per split; the
+                         // direct output when n_split == 1), summed in fixed split order
   const float* gscale;   // bwd: device scalar (upstream gradient), multiplies w
   int n_own, n_other, other_per_split, n_split;
   float inv_temp, w;
@@ -272,20 +276,46 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
       p.part[3 * stride + idx] = run_pc;
     }
   } else {
-    // transpose through LDS so each wave adds whole contiguous rows (256-B atomics)
+    // transpose through LDS so each wave stores whole contiguous rows of this split's
+    // slice (no atomics: the splits are summed in fixed order by supcon_split_reduce)
     float* out_lds = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int q = 0; q < D / 16; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) out_lds[(wv * 16 + c) * D + 16 * q + 4 * h + r] = acc2[q][r];
     __syncthreads();
+    float* slice = p.out + (size_t)blockIdx.y * p.n_own * D;
     for (int rr = 0; rr < 16; ++rr) {
       const int orow = own0 + rr;
       if (orow >= p.n_own) break;
 #pragma unroll
-      for (int d = lane; d < D; d += 64) atomicAdd(p.out + (size_t)orow * D + d, out_lds[(wv * 16 + rr) * D + d]);
+      for (int d = 4 * lane; d < D; d += 256)
+        *reinterpret_cast<float4*>(slice + (size_t)orow * D + d) =
+            *reinterpret_cast<const float4*>(out_lds + (wv * 16 + rr) * D + d);
     }
   }
+}
+
+// out[e] = Σ_{s < n_split} part[s][e] in split order (deterministic), float4 per thread
+__global__ __launch_bounds__(256) void supcon_split_reduce_kernel(const float* __restrict__ part, int n_split,
+                                                                  long n4, float* __restrict__ out) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= n4) return;
+  const float4* P = reinterpret_cast<const float4*>(part);
+  float4 a = P[e];
+  for (int s = 1; s < n_split; ++s) {
+    const float4 v = P[(size_t)s * n4 + e];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  reinterpret_cast<float4*>(out)[e] = a;
+}
+
+hipError_t split_reduce(const float* part, int n_split, long n, float* out, hipStream_t s) {
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(supcon_split_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, part, n_split,
+                     n4, out);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
 }
 
 // Combine the per-split partials: lse_i, 1/|P_i| (or -1), and the scaled loss sum.
@@ -356,6 +386,23 @@ int pick_splits(int n_own, int n_other) {
 
 int supcon_num_splits(int n_own, int n_other) { return pick_splits(n_own, n_other); }
 
+namespace {
+// the split counts the two backward passes actually use (other_per_split rounded to tiles)
+int bwd_splits(int n_own, int n_other, int* per_out) {
+  int ns = pick_splits(n_own, n_other);
+  int per = (n_other + ns - 1) / ns;
+  per = ((per + OTHER_TILE - 1) / OTHER_TILE) * OTHER_TILE;
+  *per_out = per;
+  return (n_other + per - 1) / per;
+}
+}  // namespace
+
+long supcon_bwd_workspace(int Na, int N, int D) {
+  int per;
+  const int sa = bwd_splits(Na, N, &per), sc = bwd_splits(N, Na, &per);
+  return (sa > 1 ? (long)sa * Na * D : 0) + (sc > 1 ? (long)sc * N * D : 0);
+}
+
 hipError_t launch_supcon_fwd(const float* A, const float* C, const int* a_self, const int* a_key,
                              const int* c_key, int Na, int N, int D, float inv_temp, float temp_ratio,
                              float scale, int n_split, float* part, float* lse, float* invcnt,
@@ -376,25 +423,27 @@ hipError_t launch_supcon_fwd(const float* A, const float* C, const int* a_self, 
 
 hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, const int* a_key,
                              const int* c_key, const float* lse, const float* invcnt, int Na, int N, int D,
-                             float inv_temp, float w, const float* gscale, float* dA, float* dC,
+                             float inv_temp, float w, const float* gscale, float* dA, float* dC, float* ws,
                              hipStream_t s) {
   SupconParams p{};
   p.gscale = gscale;
   p.a_self = a_self; p.a_key = a_key; p.c_key = c_key; p.lse = lse; p.invcnt = invcnt;
   p.inv_temp = inv_temp; p.w = w;
   // dA: own = anchors, other = contrasts
-  p.own = A; p.other = C; p.n_own = Na; p.n_other = N; p.out = dA;
-  p.n_split = pick_splits(Na, N);
-  int per = (N + p.n_split - 1) / p.n_split;
-  p.other_per_split = ((per + OTHER_TILE - 1) / OTHER_TILE) * OTHER_TILE;
-  p.n_split = (N + p.other_per_split - 1) / p.other_per_split;
+  p.own = A; p.other = C; p.n_own = Na; p.n_other = N;
+  p.n_split = bwd_splits(Na, N, &p.other_per_split);
+  float* ws_a = ws;
+  p.out = p.n_split > 1 ? ws_a : dA;
   hipError_t e = launch_mode<MODE_BWD_A>(D, p, s);
   if (e != hipSuccess) return e;
+  if (p.n_split > 1 && (e = split_reduce(ws_a, p.n_split, (long)Na * D, dA, s)) != hipSuccess) return e;
+  float* ws_c = ws + (p.n_split > 1 ? (long)p.n_split * Na * D : 0);
   // dC: own = contrasts, other = anchors
-  p.own = C; p.other = A; p.n_own = N; p.n_other = Na; p.out = dC;
-  p.n_split = pick_splits(N, Na);
-  per = (Na + p.n_split - 1) / p.n_split;
-  p.other_per_split = ((per + OTHER_TILE - 1) / OTHER_TILE) * OTHER_TILE;
-  p.n_split = (Na + p.other_per_split - 1) / p.other_per_split;
-  return launch_mode<MODE_BWD_C>(D, p, s);
+  p.own = C; p.other = A; p.n_own = N; p.n_other = Na;
+  p.n_split = bwd_splits(N, Na, &p.other_per_split);
+  p.out = p.n_split > 1 ? ws_c : dC;
+  e = launch_mode<MODE_BWD_C>(D, p, s);
+  if (e != hipSuccess) return e;
+  if (p.n_split > 1) return split_reduce(ws_c, p.n_split, (long)N * D, dC, s);
+  return hipSuccess;
 }
