@@ -77,6 +77,8 @@ struct IgemmParams {
   // rows stored straight from the accumulators (no bf16 rounding, no BN statistics)
   const float* bias;
   int relu, out_f32;
+  // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
+  int worder;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -171,12 +173,12 @@ struct Tile {
 // (global_load_lds) staging of both K-inner operands (FWD / DGRAD without the BN prologue):
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
-// BST (DGRAD only): 1 = fused BN-backward statistics epilogue (p.bs) — a separate variant so
+// VAR, DGRAD: 1 = fused BN-backward statistics epilogue (p.bs) — a separate variant so
 // the plain dgrad keeps its register budget. ONE (LDS-DMA, reduction <= BK): a single
 // K-tile needs no second LDS buffer; the smaller static LDS (one stage or the C tile) lets
 // twice as many blocks share a CU, hiding the load -> MFMA -> store latency of these
 // memory-bound 1x1 layer-1 GEMMs across blocks.
-template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int BST, bool ONE>
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR, bool ONE>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
   using T = Tile<MODE, BM, BN, NT>;
@@ -207,7 +209,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   const int nwg = gridDim.x;
   const int lin = xcd_remap(blockIdx.x, nwg);
   int split = 0, tile = lin;
-  if (MODE == MODE_WGRAD) { split = lin % p.splits; tile = lin / p.splits; }
+  if (MODE == MODE_WGRAD) {
+    // split-major (default): the blocks an XCD runs together are ALL output tiles of a few
+    // K-splits, so every tile re-reads the same dy / x pixel rows from that XCD's L2
+    // (tile-major put one tile's splits together: disjoint K ranges, no L2 reuse)
+    const int nt_all = p.m_tiles * p.n_tiles;
+    if (p.worder) { tile = lin % nt_all; split = lin / nt_all; }
+    else { split = lin % p.splits; tile = lin / p.splits; }
+  }
   const int mt = tile / p.n_tiles, nt = tile % p.n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
   int k_begin = 0, k_end = p.Kdim;
@@ -227,7 +236,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   const int kin_row0 = tid >> 3;
   auto a_row = [&](int i) { return GL ? 8 * (wvu * T::A_CH + i) + (lane >> 3) : kin_row0 + (NT / 8) * i; };
   auto b_row = [&](int i) { return GL ? 8 * (wvu * T::B_CH + i) + (lane >> 3) : kin_row0 + (NT / 8) * i; };
-  const bool is1x1 = (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
+  // VAR, WGRAD: bit 0 = 1x1 stride-1 unpadded filter (plain GEMM operand addressing, no
+  // pixel decode or bounds tests), bit 1 = fused BN+ReLU prologue on x (p.in_scale). Each
+  // is its own instantiation: the generic loader's address math and the prologue's
+  // registers otherwise sit in every wgrad main loop (VALU-bound: ~6-10 VALU per MFMA).
+  constexpr bool W1X1 = MODE == MODE_WGRAD && (VAR & 1);
+  constexpr bool WPRO = MODE == MODE_WGRAD && (VAR & 2);
+  const bool is1x1 = (MODE == MODE_WGRAD) ? W1X1 : (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
   // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
   // tap; DGRAD: dy coordinate of tap (r0, s0))
   int a_base[T::A_CH], a_y[T::A_CH], a_x[T::A_CH];
@@ -358,8 +373,27 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       gb_s[i] = rs - gb_r[i] * g.S;
     }
   }
+  // WGRAD generic (not 1x1) register-staged B loader: per chunk, the image index and the
+  // pixel-within-image of its row, decoded once and advanced by BK per load_tile call (the
+  // calls go in K order), instead of a division-based decode of every chunk of every tile
+  constexpr int WB = (MODE == MODE_WGRAD && !W1X1) ? T::B_CH : 1;
+  int wb_n[WB], wb_pix[WB];
+  const int wb_pq = g.P * g.Q;
+  int wb_dn = 0, wb_dpix = 0;
+  if (MODE == MODE_WGRAD && !W1X1 && !GL) {
+    wb_dn = BK / wb_pq;
+    wb_dpix = BK - wb_dn * wb_pq;
+#pragma unroll
+    for (int i = 0; i < WB; ++i) {
+      const int kk = k_begin + (tid + NT * i) / B_CPR;
+      int n, pp, qq;
+      pix_decode(kk, n, pp, qq);
+      wb_n[i] = n;
+      wb_pix[i] = kk - n * wb_pq;
+    }
+  }
   // WGRAD: fused BN+ReLU of the activation operand (channel chunk fixed per thread)
-  const bool wb_bn = (MODE == MODE_WGRAD) && p.in_scale != nullptr;
+  const bool wb_bn = WPRO && p.in_scale != nullptr;
   float wsc[8], wsh[8];
   if (wb_bn) {
     load8f(p.in_scale + wb_c, wsc);
@@ -450,11 +484,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         if (is1x1) {
           off = kk * g.C + wb_c;
         } else {
-          int n, pp, qq;
-          pix_decode(kk, n, pp, qq);
+          const int n = wb_n[i], pix = wb_pix[i];
+          const int pp = p.lq >= 0 ? pix >> p.lq : (int)fdiv((unsigned)pix, p.div_q);
+          const int qq = pix - pp * g.Q;
           const int yy = pp * g.stride - g.pad + wb_r, xx = qq * g.stride - g.pad + wb_s;
           ok = ok && (unsigned)yy < (unsigned)g.H && (unsigned)xx < (unsigned)g.W;
           off = ((n * g.H + yy) * g.W + xx) * g.C + wb_c;
+          // next K-tile: BK pixels on
+          int np = pix + wb_dpix, nn = n + wb_dn;
+          if (np >= wb_pq) { np -= wb_pq; ++nn; }
+          wb_pix[i] = np;
+          wb_n[i] = nn;
         }
         if (ok) ld_mask |= 1u << i;
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.b_elems));
@@ -751,7 +791,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   // acc[i][j][r] = C[m0 + wm*64 + 16i + c][n0 + wn*64 + 16j + 4h + r]
   // (not compiled into the BN-statistics DGRAD variant: its register budget sits at the
   // 128-VGPR occupancy step)
-  if (MODE != MODE_WGRAD && !BST && (p.bias != nullptr || p.relu)) {
+  if (MODE != MODE_WGRAD && !VAR && (p.bias != nullptr || p.relu)) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -765,7 +805,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
         }
       }
   }
-  if (MODE == MODE_WGRAD || (!BST && p.out_f32)) {
+  if (MODE == MODE_WGRAD || (!VAR && p.out_f32)) {
     // fp32 rows straight from the accumulators: 4 consecutive columns per lane (WGRAD: this
     // split's partial slab; FWD / DGRAD out_f32: stride-1 GEMM rows, host-checked)
     float* out = reinterpret_cast<float*>(p.out) + (MODE == MODE_WGRAD ? (size_t)split * p.M * p.Ncol : 0);
@@ -802,7 +842,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   constexpr int PF = ITER < 4 ? ITER : 4;
   static_assert(NT % CPR == 0 && CPR <= 64 && (BM * CPR) % NT == 0, "fixed column chunk per thread");
   const bool has_add = MODE == MODE_DGRAD && p.addend != nullptr;
-  constexpr bool bst = MODE == MODE_DGRAD && BST != 0;
+  constexpr bool bst = MODE == MODE_DGRAD && VAR != 0;
   const int my_ch = tid % CPR, my_col = n0 + my_ch * 8;
   int eo[ITER];   // output element offset of each chunk (-1: outside the tensor)
   int ea[ITER];   // addend element offset (-1: no addend there)
@@ -935,10 +975,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) d[q] = ya[q] * bmk_s[q] + bmk_t[q] > 0.f ? d[q] : 0.f;
           }
-          // BST 2: ReLU backward applied to the stored gradient too (head: dh = (dz·W2)·[h > 0]):
+          // VAR 2: ReLU backward applied to the stored gradient too (head: dh = (dz·W2)·[h > 0]):
           // the chunk is stored again, masked (bf16 values already, so the repack is exact).
           // Its own variant: the BN-statistics kernels sit at the 128-VGPR occupancy step
-          if constexpr (BST == 2) *reinterpret_cast<uint4*>(out + o) = pack8(d);
+          if constexpr (VAR == 2) *reinterpret_cast<uint4*>(out + o) = pack8(d);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             bsum[0][q] += d[q];
@@ -1097,6 +1137,14 @@ int igemm_ring() {
   return v;
 }
 
+int igemm_worder() {
+  static const int v = [] {
+    const char* e = getenv("SDX_WGRAD_ORDER");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int igemm_one() {
   static const int v = [] {
     const char* e = getenv("SDX_IGEMM_ONE");
@@ -1139,12 +1187,35 @@ hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   return hipSuccess;
 }
 
+// WGRAD launch of variant VAR (bit 0: 1x1 fast path, bit 1: BN prologue) at the depth
+// launch_cfg picks for WGRAD
+template <int BM, int BN, int WM, int WN, int VAR>
+hipError_t launch_w(int grid, const IgemmParams& p, hipStream_t s) {
+  const dim3 g(grid), b(64 * WM * WN);
+  constexpr bool kDepth2 = BM == 64 && BN == 64;
+  if (VAR < 2 && igemm_glds() == 2)
+    hipLaunchKernelGGL((igemm_kernel<MODE_WGRAD, BM, BN, WM, WN, 3, VAR, false>), g, b, 0, s, p);
+  else if (kDepth2 && igemm_depth() == 2)
+    hipLaunchKernelGGL((igemm_kernel<MODE_WGRAD, BM, BN, WM, WN, kDepth2 ? 2 : 1, VAR, false>), g, b, 0, s, p);
+  else
+    hipLaunchKernelGGL((igemm_kernel<MODE_WGRAD, BM, BN, WM, WN, 1, VAR, false>), g, b, 0, s, p);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 template <int MODE, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   p.ablate = igemm_ablate();
   p.m_tiles = (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
   const int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
+  if constexpr (MODE == MODE_WGRAD) {
+    const ConvGeom& g = p.g;
+    const bool k1 = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+    if (p.in_scale != nullptr) return launch_w<BM, BN, WM, WN, 2>(grid, p, s);
+    if (k1) return launch_w<BM, BN, WM, WN, 1>(grid, p, s);
+    return launch_w<BM, BN, WM, WN, 0>(grid, p, s);
+  } else {
   // depth 2 only where the second register stage fits without spilling (checked with
   // -Rpass-analysis=kernel-resource-usage)
   constexpr bool kDepth2 = (BM == 64 && BN == 64) || (MODE == MODE_FWD && BM != 256);
@@ -1167,6 +1238,7 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
     }
   }
   return launch_k<MODE, BM, BN, WM, WN, 1>(bs, grid, p, s);
+  }
 }
 
 // tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
@@ -1303,6 +1375,7 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
     while ((1 << l) < v) ++l;
     return (1 << l) == v ? l : -1;
   };
+  p.worder = igemm_worder();
   p.lq = log2_exact(g.Q);
   p.lpq = log2_exact(g.P * g.Q);
   if (p.lq < 0 || p.lpq < 0) p.lq = p.lpq = -1;
