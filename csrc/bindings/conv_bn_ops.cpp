@@ -172,13 +172,16 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     for (int pw = 0; pw < stride; ++pw) {
       int r0, nr, s0, ns, Hc, Wc;
       conv_dgrad_class(g, ph, pw, &r0, &nr, &s0, &ns, &Hc, &Wc);
-      torch::Tensor wc;
-      if (nr > 0 && ns > 0)
-        wc = wt.slice(1, r0, g.R, stride).slice(2, s0, g.S, stride).contiguous();
-      else
-        wc = wt;   // no taps: the kernel writes zeros and never reads B
+      // the class taps are read in place from the full weight (no per-class slice copy;
+      // a class with no taps writes zeros and never reads B). SDX_DGRAD_WFULL=0: copies.
+      static const bool wfull = [] {
+        const char* e = getenv("SDX_DGRAD_WFULL");
+        return e == nullptr || atoi(e) != 0;
+      }();
+      torch::Tensor wc = wt;
+      if (!wfull && nr > 0 && ns > 0) wc = wt.slice(1, r0, g.R, stride).slice(2, s0, g.S, stride).contiguous();
       check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                        cur_stream(), amask, bs, add ? (int)addend_sub : 0),
+                                        cur_stream(), amask, bs, add ? (int)addend_sub : 0, nullptr, wfull ? 1 : 0),
                 "conv_dgrad(class)");
       if (bs) bs->row0 += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
     }
@@ -269,7 +272,12 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   if (splits <= 0) {
     const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
                           ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
-    splits = std::max<int64_t>(1, 512 / tiles);
+    // blocks per wgrad launch (SDX_WGRAD_TARGET, default 512 = 2 per CU)
+    static const int64_t target = [] {
+      const char* e = getenv("SDX_WGRAD_TARGET");
+      return e ? std::max<int64_t>(64, atoll(e)) : (int64_t)512;
+    }();
+    splits = std::max<int64_t>(1, target / tiles);
     const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
     splits = std::min(splits, max_splits);
     // bound the fp32 partial slab to ~64 MiB, and to ~16 MiB / 256 splits for 1x1 GEMMs with

@@ -66,13 +66,14 @@ int igemm_tile_n(int cfg);
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr,
                            const GemmEpi* epi = nullptr);
-// strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous)
+// strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous),
+// or (wt_full) the whole dgrad weight Wt [C][R][S][K], the class taps addressed in place
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                    const BnBwdStat* bstat = nullptr, int addend_sub = 0,
-                                   const GemmEpi* epi = nullptr);
+                                   const GemmEpi* epi = nullptr, int wt_full = 0);
 // M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
 int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);

@@ -79,6 +79,10 @@ struct IgemmParams {
   int relu, out_f32;
   // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
   int worder;
+  // DGRAD sub-pixel class of a strided conv: b_rsk = R*S*K > 0 means B is the FULL dgrad
+  // weight Wt [C][R][S][K] and the class taps r = r0 + st*ir, s = s0 + st*is are addressed
+  // in place (no per-class contiguous copy of the tap slice); 0: B = [Ncol][Kdim] as is
+  int b_rsk;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -285,7 +289,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const int col = n0 + b_row(i);
-      b_off[i] = col < p.Ncol ? col * p.Kdim : -1;
+      b_off[i] = col < p.Ncol ? col * (p.b_rsk > 0 ? p.b_rsk : p.Kdim) : -1;
     }
     const int k = k_begin + kin_ch * 8;
     kc = k % cdim;
@@ -293,6 +297,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     kr = rs / tap_s;
     ks = rs - kr * tap_s;
   }
+  // B column offset of the k chunk decoded as (kc, ks, kr): k itself, or in a full strided
+  // dgrad weight the class tap (r0 + st*kr, s0 + st*ks)
+  auto b_koff = [&](int k, int kc_, int ks_, int kr_) {
+    if (MODE == MODE_DGRAD && p.b_rsk > 0)
+      return ((p.r0 + g.stride * kr_) * g.S + p.s0 + g.stride * ks_) * g.K + kc_;
+    return k;
+  };
   // Uniform-tap fast path of the LDS-DMA loader: when the channel dim is a multiple of BK
   // every K-tile lies inside one filter tap, so the tap (and the channel base) is
   // wave-uniform: per-row validity over all taps is precomputed as a bitmask and a chunk
@@ -453,8 +464,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       // B: weights [Ncol][Kdim] K-contiguous
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + k + 8 <= p.b_elems);
-        rb[i] = ld16_or_zero(p.b + b_off[i] + k, kok && b_off[i] >= 0);
+        const int bk = b_koff(k, kc, ks, kr);
+        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + bk + 8 <= p.b_elems);
+        rb[i] = ld16_or_zero(p.b + b_off[i] + bk, kok && b_off[i] >= 0);
       }
       // advance the k decode by one tile
       kc += BK;
@@ -564,8 +576,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
         const bool ok = kok && b_off[i] >= 0;
-        SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
+        const int bk = b_koff(k, u_c0 + lane_c, u_ks, u_kr);
+        SDX_DCHECK(!ok || (long)b_off[i] + bk + 8 <= p.b_elems);
+        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + bk) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -598,8 +611,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const bool ok = kok && b_off[i] >= 0;
-      SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
+      const int bk = b_koff(k, kc, ks, kr);
+      SDX_DCHECK(!ok || (long)b_off[i] + bk + 8 <= p.b_elems);
+      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + bk) : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                        16, 0, 0);
@@ -1316,8 +1330,9 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
-                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi) {
+                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi, int wt_full) {
   IgemmParams p{};
+  p.b_rsk = (wt_full && g.stride > 1) ? g.R * g.S * g.K : 0;
   set_epi(p, epi);
   if (p.out_f32 && (g.stride != 1 || addend != nullptr || (bstat != nullptr && bstat->slab != nullptr)))
     return hipErrorInvalidValue;
@@ -1337,7 +1352,7 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   p.Ncol = g.C;
   p.Kdim = p.nr * p.ns * g.K;
   p.a_elems = (long)g.N * g.P * g.Q * g.K;
-  p.b_elems = (long)p.Ncol * p.Kdim;
+  p.b_elems = (long)p.Ncol * (p.b_rsk > 0 ? p.b_rsk : p.Kdim);
   return launch_any<MODE_DGRAD>(p, cfg, s);
 }
 
