@@ -16,6 +16,8 @@ def main():
     d = sys.argv[1]
     f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
+    for r in rows:
+        r["Kernel_Name"] = r["Kernel_Name"].replace("(anonymous namespace)::", "")
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
     a, b = idx[-2], idx[-1]
@@ -43,6 +45,25 @@ def main():
     print("largest gaps (us, at us into the step, after -> before):")
     for g, at, pn, nn in sorted(where, reverse=True)[:15]:
         print(f"  {g:7.1f} @{at:8.1f}  {pn.split('(')[0]}  ->  {nn.split('(')[0]}")
+    # per-stream busy time in the step (union per stream) and their overlap
+    key = next((k for k in ("Stream_Id", "Queue_Id", "Stream_ID", "Queue_ID") if k in rows[0]), None)
+    if key:
+        by = defaultdict(list)
+        for r in rows[a + 1:b + 1]:
+            by[r[key]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+        print(f"per {key}: busy us (kernels)")
+        for q, iv in sorted(by.items(), key=lambda kv: -len(kv[1])):
+            iv.sort()
+            tot, c = 0, t0
+            for s0, e0, _ in iv:
+                if e0 > c:
+                    tot += e0 - max(s0, c)
+                    c = e0
+            top = defaultdict(float)
+            for s0, e0, n in iv:
+                top[n.split("(")[0].replace("void ", "")[:40]] += (e0 - s0) / 1e3
+            tops = ", ".join(f"{k} {v:.0f}" for k, v in sorted(top.items(), key=lambda kv: -kv[1])[:3])
+            print(f"  {q}: {tot / 1e3:8.1f} us ({len(iv)})  {tops}")
 
 
 if __name__ == "__main__":
