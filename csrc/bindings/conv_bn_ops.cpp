@@ -77,8 +77,75 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
 
 namespace {
 
-std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
-                                    int64_t cfg, OptT in_scale, OptT in_shift) {
+// In-kernel BN-statistics reduction (StatFuse, launchers.h) requested by a caller of
+// conv_fwd_impl / conv_dgrad_bnstat_impl: the per-channel epilogue (0 sums only — SyncBN
+// all-reduces next, 1 BN finalize, 2 BN-backward coefficients) runs in the conv's last
+// block; `sums` ([nsets][C] fp64) is filled in. Replaces a column-reduce launch per BN.
+struct FuseReq {
+  int epi = 0;
+  BnFinalizeArgs fa{};
+  BnCoefArgs ca{};
+  torch::Tensor sums;
+};
+
+// SDX_STAT_FUSE bits (or stat_fuse_set): 1 forward convs, 2 backward dgrads. Default 0
+// (separate column-reduce launches): measured 13.84 vs 14.02 ms/step with both bits on the
+// same box — the last arriver's serial reduction of ~sqrt(m_tiles) slab rows lands on each
+// conv's critical tail and costs as much as the wide reduction launch it replaces
+// (profiles/ablate_reduce_r2.txt).
+std::atomic<int>& stat_fuse_flag() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("SDX_STAT_FUSE");
+    return e == nullptr ? 0 : atoi(e);
+  }()};
+  return on;
+}
+
+bool stat_fuse_enabled(int bit) { return (stat_fuse_flag().load(std::memory_order_relaxed) & bit) != 0; }
+
+int64_t stat_fuse_set(int64_t bits) { return stat_fuse_flag().exchange((int)bits); }
+
+// ticket counters of the in-kernel reduction: zeroed once per device, reset by the kernels'
+// last arrivers; rotating slots (as reduce_counters) so launches on different streams never
+// share one
+unsigned* fuse_counters(const torch::Device& dev, int n) {
+  constexpr int kSlots = 128, kPerSlot = 8192;
+  TORCH_CHECK(n >= 1 && n <= kPerSlot, "StatFuse: ", n, " counters exceed a slot");
+  static std::mutex mu;
+  static std::map<int, std::pair<torch::Tensor, int>> pool;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = pool[dev.index()];
+  if (!e.first.defined())
+    e.first = torch::zeros({kSlots * kPerSlot}, torch::TensorOptions().dtype(at::kInt).device(dev));
+  const int slot = e.second;
+  e.second = (slot + 1) % kSlots;
+  return reinterpret_cast<unsigned*>(e.first.data_ptr<int>()) + slot * kPerSlot;
+}
+
+// StatFuse plan of an M x Ncol GEMM run with tile config cfg; lvl2 keeps the level-2 rows
+// alive until the call returns (stream-ordered reuse by the caching allocator)
+StatFuse make_fuse(FuseReq& r, const torch::Tensor& like, int64_t M, int64_t Ncol, int cfg, int nsets,
+                   torch::Tensor& lvl2) {
+  const int mt = (int)((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg));
+  const int nt = (int)((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
+  StatFuse f{};
+  f.group = stat_fuse_groups(mt);
+  f.n_groups = (mt + f.group - 1) / f.group;
+  f.cnt = fuse_counters(like.device(), stat_fuse_counters(mt, nt));
+  auto dopt = like.options().dtype(at::kDouble);
+  lvl2 = torch::empty({(int64_t)f.n_groups * nsets * Ncol}, dopt);
+  r.sums = torch::empty({nsets, Ncol}, dopt);
+  f.lvl2 = lvl2.data_ptr<double>();
+  f.sums = r.sums.data_ptr<double>();
+  f.epi = r.epi;
+  f.fa = r.fa;
+  f.ca = r.ca;
+  return f;
+}
+
+std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad,
+                                         bool want_stats, int64_t cfg, OptT in_scale, OptT in_shift,
+                                         FuseReq* fr) {
   check_bf16_nhwc(x, "x");
   check_bf16_nhwc(w, "w");
   TORCH_CHECK(w.size(3) == x.size(3), "weight Cin != input C");
@@ -106,15 +173,28 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
   }
   const float *isc, *ish;
   in_bn_ptrs(in_scale, in_shift, g.C, &isc, &ish);
-  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream(), isc, ish),
+  StatFuse sf{};
+  torch::Tensor lvl2;
+  if (fr != nullptr) {
+    TORCH_CHECK(want_stats && isc == nullptr, "StatFuse: statistics without the BN prologue only");
+    sf = make_fuse(*fr, x, M, g.K, (int)cfg, 2, lvl2);
+  }
+  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream(), isc, ish,
+                            nullptr, fr != nullptr ? &sf : nullptr),
             "conv_fwd");
   return {y, slab};
+}
+
+std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
+                                    int64_t cfg, OptT in_scale, OptT in_shift) {
+  return conv_fwd_impl(x, w, stride, pad, want_stats, cfg, in_scale, in_shift, nullptr);
 }
 
 // bs (optional): fused BN-backward statistics; its slab must hold conv_dgrad_slab_rows rows
 torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                               int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
-                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0) {
+                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0,
+                              FuseReq* fr = nullptr) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
   TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
@@ -161,9 +241,14 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     amask = addend_mask->data_ptr();
   }
   if (bs) bs->row0 = 0;
+  TORCH_CHECK(fr == nullptr || (bs != nullptr && stride == 1), "StatFuse: single-launch statistics dgrads only");
   if (stride == 1) {
+    StatFuse sf{};
+    torch::Tensor lvl2;
+    if (fr != nullptr) sf = make_fuse(*fr, dy, M, g.C, (int)cfg, bs->yb != nullptr ? 3 : 2, lvl2);
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0),
+                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0, nullptr,
+                                      fr != nullptr ? &sf : nullptr),
               "conv_dgrad");
     return dx;
   }
@@ -172,16 +257,13 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     for (int pw = 0; pw < stride; ++pw) {
       int r0, nr, s0, ns, Hc, Wc;
       conv_dgrad_class(g, ph, pw, &r0, &nr, &s0, &ns, &Hc, &Wc);
-      // the class taps are read in place from the full weight (no per-class slice copy;
-      // a class with no taps writes zeros and never reads B). SDX_DGRAD_WFULL=0: copies.
-      static const bool wfull = [] {
-        const char* e = getenv("SDX_DGRAD_WFULL");
-        return e == nullptr || atoi(e) != 0;
-      }();
-      torch::Tensor wc = wt;
-      if (!wfull && nr > 0 && ns > 0) wc = wt.slice(1, r0, g.R, stride).slice(2, s0, g.S, stride).contiguous();
+      torch::Tensor wc;
+      if (nr > 0 && ns > 0)
+        wc = wt.slice(1, r0, g.R, stride).slice(2, s0, g.S, stride).contiguous();
+      else
+        wc = wt;   // no taps: the kernel writes zeros and never reads B
       check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                        cur_stream(), amask, bs, add ? (int)addend_sub : 0, nullptr, wfull ? 1 : 0),
+                                        cur_stream(), amask, bs, add ? (int)addend_sub : 0),
                 "conv_dgrad(class)");
       if (bs) bs->row0 += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
     }
@@ -197,10 +279,11 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t 
 // dgrad + fused BN-backward statistics of dx for the BN whose pre-BN tensor is ya (and yb,
 // a second BN fed by the same gradient: projection shortcut). ReLU mask from `mask_bits`
 // (1 bit per element) or recomputed as ya·msc + msh > 0. Returns [dx, slab [rows][2|3][C]].
-std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W,
-                                             int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
-                                             OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
-                                             OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0) {
+std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W,
+                                                  int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
+                                                  OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb,
+                                                  OptT mb, OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub,
+                                                  FuseReq* fr) {
   check_bf16_nhwc(ya, "ya");
   const int64_t C = wt.size(0);
   TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
@@ -240,8 +323,16 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
   const int ns = yb.has_value() ? 3 : 2;
   auto slab = torch::empty({rows, ns, C}, dy.options().dtype(at::kFloat));
   bs.slab = slab.data_ptr<float>();
-  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs, addend_sub);
+  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs, addend_sub, fr);
   return {dx, slab};
+}
+
+std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W,
+                                             int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
+                                             OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
+                                             OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0) {
+  return conv_dgrad_bnstat_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, ya, ma, yb, mb, mask_bits,
+                                msc, msh, addend_sub, nullptr);
 }
 
 }  // namespace
@@ -272,12 +363,7 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   if (splits <= 0) {
     const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
                           ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
-    // blocks per wgrad launch (SDX_WGRAD_TARGET, default 512 = 2 per CU)
-    static const int64_t target = [] {
-      const char* e = getenv("SDX_WGRAD_TARGET");
-      return e ? std::max<int64_t>(64, atoll(e)) : (int64_t)512;
-    }();
-    splits = std::max<int64_t>(1, target / tiles);
+    splits = std::max<int64_t>(1, 512 / tiles);
     const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
     splits = std::min(splits, max_splits);
     // bound the fp32 partial slab to ~64 MiB, and to ~16 MiB / 256 splits for 1x1 GEMMs with
@@ -712,6 +798,34 @@ BnState bn_forward(const torch::Tensor& slab, double count, const torch::Tensor&
 
 double rows_of(const torch::Tensor& y) { return (double)(y.numel() / y.size(3)); }
 
+// conv + BN forward statistics. Training with StatFuse: the conv's last block reduces the
+// statistics and (one rank) finalizes the BN in the same launch; SyncBN: it leaves the sums
+// for the in-place all-reduce, then one finalize launch.
+std::pair<torch::Tensor, BnState> conv_bn_fwd(const torch::Tensor& x, const torch::Tensor& w, int64_t stride,
+                                              int64_t pad, const torch::Tensor& g, const torch::Tensor& b,
+                                              const torch::Tensor& rm, const torch::Tensor& rv, double eps,
+                                              double mom, bool training, int64_t comm) {
+  if (!training || !stat_fuse_enabled(1)) {
+    auto c = conv_fwd(x, w, stride, pad, training, -1, c10::nullopt, c10::nullopt);
+    return {c[0], bn_forward(c[1], rows_of(c[0]), g, b, rm, rv, eps, mom, training, comm)};
+  }
+  const bool sync = comm != 0 && small_comm_world(comm) > 1;
+  FuseReq fr;
+  FinalizeOut o;
+  const int64_t C = w.size(0);
+  if (!sync) {
+    // count: output rows; known before the launch from the geometry
+    const int64_t P = (x.size(1) + 2 * pad - w.size(1)) / stride + 1, Q = (x.size(2) + 2 * pad - w.size(2)) / stride + 1;
+    fr.epi = 1;
+    fr.fa = finalize_args(x, C, (double)(x.size(0) * P * Q), g, b, eps, mom, true, rm, rv, o);
+  }
+  auto c = conv_fwd_impl(x, w, stride, pad, true, -1, c10::nullopt, c10::nullopt, &fr);
+  if (!sync) return {c[0], BnState{o.scale, o.shift, o.mean, o.invstd}};
+  small_all_reduce_(comm, fr.sums);
+  auto r = bn_finalize(fr.sums, rows_of(c[0]) * small_comm_world(comm), g, b, eps, mom, true, rm, rv);
+  return {c[0], BnState{r[0], r[1], r[2], r[3]}};
+}
+
 // bn_bwd_reduce_coef, or (communicator of >1 ranks) reduce -> in-place all-reduce of the
 // [Σdz, Σdz·y(, Σdz·y_b)] sums -> coefficients, with count scaled to the global row count
 std::vector<torch::Tensor> bn_bwd_sync(int64_t comm, torch::Tensor dout, OptT outv, torch::Tensor ya,
@@ -831,21 +945,19 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   std::vector<BnState> st;
   std::vector<torch::Tensor> out(7);
   const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
-  auto c1 = conv_fwd(x, w[0], s1, p1, training, -1, c10::nullopt, c10::nullopt);
-  const double cnt1 = rows_of(c1[0]);
-  st.push_back(bn_forward(c1[1], cnt1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training, comm));
-  auto a1 = bn_apply(c1[0], st[0].sc, st[0].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
+  auto c1 = conv_bn_fwd(x, w[0], s1, p1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training, comm);
+  st.push_back(c1.second);
+  auto a1 = bn_apply(c1.first, st[0].sc, st[0].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
   const int64_t s2 = bottleneck ? stride : 1;
-  auto c2 = conv_fwd(a1, w[1], s2, 1, training, -1, c10::nullopt, c10::nullopt);
-  const double cnt2 = rows_of(c2[0]);
-  st.push_back(bn_forward(c2[1], cnt2, B(1, 0), B(1, 1), B(1, 2), B(1, 3), eps, momentum, training, comm));
-  torch::Tensor last = c2[0], a2;
+  auto c2 = conv_bn_fwd(a1, w[1], s2, 1, B(1, 0), B(1, 1), B(1, 2), B(1, 3), eps, momentum, training, comm);
+  st.push_back(c2.second);
+  torch::Tensor last = c2.first, a2;
   int lastbn = 1;
   if (bottleneck) {
-    a2 = bn_apply(c2[0], st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
-    auto c3 = conv_fwd(a2, w[2], 1, 0, training, -1, c10::nullopt, c10::nullopt);
-    st.push_back(bn_forward(c3[1], cnt2, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm));
-    last = c3[0];
+    a2 = bn_apply(c2.first, st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
+    auto c3 = conv_bn_fwd(a2, w[2], 1, 0, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm);
+    st.push_back(c3.second);
+    last = c3.first;
     lastbn = 2;
   }
   torch::Tensor o, ys;
@@ -854,19 +966,19 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
                                  : torch::Tensor();
   const OptT om = training ? OptT(omask) : OptT();
   if (proj) {
-    auto cs = conv_fwd(x, w[nconv], stride, 0, training, -1, c10::nullopt, c10::nullopt);
-    st.push_back(bn_forward(cs[1], cnt2, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
-                            training, comm));
-    ys = cs[0];
+    auto cs = conv_bn_fwd(x, w[nconv], stride, 0, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
+                          training, comm);
+    st.push_back(cs.second);
+    ys = cs.first;
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true, om);
   } else {
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, x, c10::nullopt, c10::nullopt, 2, true, om);
   }
   out.push_back(omask);    // index 7 (before the per-BN state)
   out[0] = o;
-  out[1] = c1[0];
+  out[1] = c1.first;
   out[2] = a1;
-  out[3] = c2[0];
+  out[3] = c2.first;
   out[4] = bottleneck ? a2 : torch::Tensor();
   out[5] = bottleneck ? last : torch::Tensor();
   out[6] = ys;
@@ -939,6 +1051,26 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   // Σda·m, Σda·m·(y−μ) come from the dgrad epilogue (SDX_DGRAD_BNSTAT=0: separate pass)
   auto dgrad_bn = [&](const torch::Tensor& dyo, const torch::Tensor& w, const torch::Tensor& y, int64_t st,
                       int64_t pad, int i, double cnt) -> std::pair<torch::Tensor, torch::Tensor> {
+    if (dgrad_bnstat_enabled() && st == 1 && stat_fuse_enabled(2)) {
+      // the dgrad's last block reduces the statistics and (one rank) evaluates the coefficients
+      const bool sync = comm != 0 && small_comm_world(comm) > 1;
+      FuseReq fr;
+      CoefOut o;
+      if (!sync) {
+        fr.epi = 2;
+        fr.ca = coef_args(y, y.size(3), 1, cnt, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt, c10::nullopt,
+                          G(i, 1), G(i, 2), c10::nullopt, c10::nullopt, o);
+      }
+      auto r = conv_dgrad_bnstat_impl(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt,
+                                      c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0),
+                                      S(i, 1), 0, &fr);
+      if (!sync) return {r[0], o.coef_a};
+      small_all_reduce_(comm, fr.sums);
+      const int wsz = small_comm_world(comm);
+      auto c = bn_bwd_coef(fr.sums, cnt * wsz, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt, c10::nullopt,
+                           G(i, 1), G(i, 2), c10::nullopt, c10::nullopt, 1.0 / wsz);
+      return {r[0], c[0]};
+    }
     if (dgrad_bnstat_enabled()) {
       auto r = conv_dgrad_bnstat(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt,
                                  c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0), S(i, 1));
@@ -1007,6 +1139,10 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
 }  // namespace
 
 void register_conv_bn(pybind11::module& m) {
+  m.def("stat_fuse_set", &stat_fuse_set,
+        "in-kernel BN-statistics reduction of the block executor (bits: 1 forward, 2 backward); returns the "
+        "previous bits",
+        pybind11::arg("bits"));
   m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16) + BN stat slab [+ BN+ReLU prologue]",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("want_stats"), pybind11::arg("cfg") = -1, pybind11::arg("in_scale") = pybind11::none(),

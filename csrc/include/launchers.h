@@ -63,17 +63,21 @@ struct GemmEpi {
 int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
+struct StatFuse;
+// sf (optional, with stats): reduce the statistics slab in-kernel (StatFuse)
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr,
-                           const GemmEpi* epi = nullptr);
-// strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous),
-// or (wt_full) the whole dgrad weight Wt [C][R][S][K], the class taps addressed in place
+                           const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);
+// strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous)
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                    const BnBwdStat* bstat = nullptr, int addend_sub = 0,
-                                   const GemmEpi* epi = nullptr, int wt_full = 0);
+                                   const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);
+// in-kernel statistics reduction plan for an M x Ncol GEMM of tile config cfg
+int stat_fuse_groups(int m_tiles);
+int stat_fuse_counters(int m_tiles, int n_tiles);
 // M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
 int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
@@ -107,6 +111,24 @@ struct BnCoefArgs {
   // bucket reducer's sum × 1/W yields global / W and not the global value.
   double grad_scale = 1.0;
 };
+// In-kernel reduction of a conv GEMM's per-M-tile BN statistics (igemm.hip), replacing the
+// separate column-reduce launch: every block stores its slab row write-through, drains and
+// takes a ticket on its (M-tile group, N-tile) counter; a group's last arriver sums the
+// group's rows (fp64, row order) into a level-2 row and tickets its N-tile counter; the last
+// of those sums the level-2 rows (group order) into `sums` and runs the per-channel epilogue
+// for its columns. Deterministic for any dispatch order or XCD placement.
+struct StatFuse {
+  unsigned* cnt;     // [n_groups * n_tiles] level-1 then [n_tiles] level-2 tickets; zero on
+                     // entry, reset by their last arriver (nullptr: no fusion, slab only)
+  double* lvl2;      // [n_groups][nsets][Ncol]
+  double* sums;      // [nsets][Ncol]
+  int group;         // M-tiles per level-1 group
+  int n_groups;
+  int epi;           // 0 sums only (SyncBN: all-reduce next), 1 BN finalize, 2 BN-bwd coefficients
+  BnFinalizeArgs fa;
+  BnCoefArgs ca;
+};
+
 // Deterministic reduction of a [rows][nsets][C] fp32 slab to fp64 sums [nsets][C] in ONE
 // launch (per-block partials + last-arriver combine; no memset). epi: 0 sums only,
 // 1 + BN finalize (nsets 2), 2 + BN backward coefficients (nsets 2|3), 3 gradient-sink add

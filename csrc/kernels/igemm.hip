@@ -29,6 +29,7 @@
 // by igemm_splitk_reduce), never atomics. Block→tile order is XCD-aware.
 #include "common.h"
 #include "launchers.h"
+#include "bn_epilogue.h"
 
 using namespace sdx;
 
@@ -79,10 +80,8 @@ struct IgemmParams {
   int relu, out_f32;
   // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
   int worder;
-  // DGRAD sub-pixel class of a strided conv: b_rsk = R*S*K > 0 means B is the FULL dgrad
-  // weight Wt [C][R][S][K] and the class taps r = r0 + st*ir, s = s0 + st*is are addressed
-  // in place (no per-class contiguous copy of the tap slice); 0: B = [Ncol][Kdim] as is
-  int b_rsk;
+  // FWD statistics / DGRAD BN-backward statistics reduced in-kernel (sf.cnt != nullptr)
+  StatFuse sf;
   int M, Ncol, Kdim;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
@@ -173,17 +172,145 @@ struct Tile {
   static constexpr int B_CH = BN * BK / 8 / NT;
 };
 
+// write-through (sc1) fp32 / fp64 stores and loads of the statistics hand-off
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// StatFuse tail (launchers.h): run by every thread of a block right after its slab row
+// (row `mt` of [m_tiles][NS][Ncol], stored sc1) is written. Hand-off protocol as in bn.hip
+// col_reduce: every storing wave drains its sc1 stores, a barrier, ONE lane's agent-scope
+// ticket; only the last arriver reads the handed-off rows, all with sc1 loads. Inlined: it
+// runs after the accumulators are dead (a call would impose the ABI: scratch + spills).
+template <int NT, int BN, int NS>
+__device__ __forceinline__ void stat_fuse_tail(const StatFuse& f, const float* slab, int Ncol, int mt, int m_tiles,
+                                            int nt, int n_tiles, int n0, unsigned char* smem) {
+  constexpr int P = NT / BN;                 // row parts per column (NT >= BN for every tile)
+  static_assert(P >= 1 && P * BN == NT, "thread (column, part) layout");
+  const int tid = threadIdx.x, col = tid % BN, part = tid / BN;
+  int* flag = reinterpret_cast<int*>(smem);
+  double* red = reinterpret_cast<double*>(smem + 16);   // [P][NS][BN]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int g = mt / f.group;
+  const int r0 = g * f.group, r1 = min(m_tiles, r0 + f.group);
+  unsigned* c1 = f.cnt + g * n_tiles + nt;
+  unsigned* c2 = f.cnt + f.n_groups * n_tiles + nt;
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = t == (unsigned)(r1 - r0 - 1);
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const bool cok = n0 + col < Ncol;
+  // level 1: part p sums the group's rows r0+p, r0+p+P, ... (4 rows in flight), fp64
+  {
+    double acc[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acc[k] = 0.0;
+    if (cok) {
+      const size_t rs = (size_t)NS * Ncol;              // slab row stride (floats)
+      const float* q = slab + (size_t)(r0 + part) * rs + n0 + col;
+      int r = r0 + part;
+      for (; r + 3 * P < r1; r += 4 * P, q += 4 * P * rs) {
+        float v[4][NS];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int k = 0; k < NS; ++k) v[u][k] = ld_sc1(q + u * P * rs + (size_t)k * Ncol);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int k = 0; k < NS; ++k) acc[k] += (double)v[u][k];
+      }
+      for (; r < r1; r += P, q += P * rs)
+#pragma unroll
+        for (int k = 0; k < NS; ++k) acc[k] += (double)ld_sc1(q + (size_t)k * Ncol);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) red[(part * NS + k) * BN + col] = acc[k];
+    __syncthreads();
+    if (part == 0 && cok) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        double t = 0.0;
+        for (int q = 0; q < P; ++q) t += red[(q * NS + k) * BN + col];
+        st_sc1(f.lvl2 + ((size_t)g * NS + k) * Ncol + n0 + col, t);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(c1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+    const unsigned t = __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[1] = t == (unsigned)(f.n_groups - 1);
+  }
+  __syncthreads();
+  if (!flag[1]) return;
+  // level 2: part p sums groups p, p+P, ... in order, then the parts in order
+  {
+    double acc[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acc[k] = 0.0;
+    if (cok)
+      for (int q = part; q < f.n_groups; q += P)
+#pragma unroll
+        for (int k = 0; k < NS; ++k) acc[k] += ld_sc1(f.lvl2 + ((size_t)q * NS + k) * Ncol + n0 + col);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) red[(part * NS + k) * BN + col] = acc[k];
+    __syncthreads();
+    if (part == 0 && cok) {
+      double t[NS];
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        t[k] = 0.0;
+        for (int q = 0; q < P; ++q) t[k] += red[(q * NS + k) * BN + col];
+        f.sums[(size_t)k * Ncol + n0 + col] = t[k];
+      }
+      if constexpr (NS == 2) {
+        if (f.epi == 1) bn_finalize_one(n0 + col, t[0], t[1], f.fa);
+      }
+      if (f.epi == 2) bn_coef_one(n0 + col, Ncol, t, NS - 1, f.ca);
+    }
+  }
+  if (tid == 0) __hip_atomic_store(c2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // DEPTH: 1 / 2 = register-staged operands, 1 or 2 K-tiles of prefetch; 3 = LDS-DMA
 // (global_load_lds) staging of both K-inner operands (FWD / DGRAD without the BN prologue):
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
 // VAR, DGRAD: 1 = fused BN-backward statistics epilogue (p.bs) — a separate variant so
-// the plain dgrad keeps its register budget. ONE (LDS-DMA, reduction <= BK): a single
+// the plain dgrad keeps its register budget; 3 = the same plus the in-kernel statistics
+// reduction (p.sf, StatFuse). VAR, FWD: 1 = in-kernel reduction of the BN statistics slab
+// (p.sf). ONE (LDS-DMA, reduction <= BK): a single
 // K-tile needs no second LDS buffer; the smaller static LDS (one stage or the C tile) lets
 // twice as many blocks share a CU, hiding the load -> MFMA -> store latency of these
 // memory-bound 1x1 layer-1 GEMMs across blocks.
+// waves/SIMD the register allocator must fit: the StatFuse dgrad variants are held to the
+// occupancy of their plain statistics variant (the tail would otherwise cost one wave)
+template <int MODE, int BM, int BN, int WM, int WN, int VAR>
+constexpr int igemm_min_waves() {
+  if (MODE != MODE_DGRAD || VAR != 3) return 2;
+  if (BM == 64 && BN == 64) return 5;
+  return (BM == 128 && BN == 128 && WM * WN == 8) ? 4 : 2;   // the others are at 2 (or 1) anyway
+}
+
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR, bool ONE>
-__global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
+__global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN, VAR>())) void igemm_kernel(IgemmParams p) {
   constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
   using T = Tile<MODE, BM, BN, NT>;
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
@@ -246,6 +373,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
   // registers otherwise sit in every wgrad main loop (VALU-bound: ~6-10 VALU per MFMA).
   constexpr bool W1X1 = MODE == MODE_WGRAD && (VAR & 1);
   constexpr bool WPRO = MODE == MODE_WGRAD && (VAR & 2);
+  constexpr bool SF = (MODE == MODE_FWD && VAR == 1) || (MODE == MODE_DGRAD && VAR == 3);
   const bool is1x1 = (MODE == MODE_WGRAD) ? W1X1 : (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
   // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
   // tap; DGRAD: dy coordinate of tap (r0, s0))
@@ -289,7 +417,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const int col = n0 + b_row(i);
-      b_off[i] = col < p.Ncol ? col * (p.b_rsk > 0 ? p.b_rsk : p.Kdim) : -1;
+      b_off[i] = col < p.Ncol ? col * p.Kdim : -1;
     }
     const int k = k_begin + kin_ch * 8;
     kc = k % cdim;
@@ -297,13 +425,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     kr = rs / tap_s;
     ks = rs - kr * tap_s;
   }
-  // B column offset of the k chunk decoded as (kc, ks, kr): k itself, or in a full strided
-  // dgrad weight the class tap (r0 + st*kr, s0 + st*ks)
-  auto b_koff = [&](int k, int kc_, int ks_, int kr_) {
-    if (MODE == MODE_DGRAD && p.b_rsk > 0)
-      return ((p.r0 + g.stride * kr_) * g.S + p.s0 + g.stride * ks_) * g.K + kc_;
-    return k;
-  };
   // Uniform-tap fast path of the LDS-DMA loader: when the channel dim is a multiple of BK
   // every K-tile lies inside one filter tap, so the tap (and the channel base) is
   // wave-uniform: per-row validity over all taps is precomputed as a bitmask and a chunk
@@ -464,9 +585,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       // B: weights [Ncol][Kdim] K-contiguous
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        const int bk = b_koff(k, kc, ks, kr);
-        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + bk + 8 <= p.b_elems);
-        rb[i] = ld16_or_zero(p.b + b_off[i] + bk, kok && b_off[i] >= 0);
+        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + k + 8 <= p.b_elems);
+        rb[i] = ld16_or_zero(p.b + b_off[i] + k, kok && b_off[i] >= 0);
       }
       // advance the k decode by one tile
       kc += BK;
@@ -576,9 +696,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
         const bool ok = kok && b_off[i] >= 0;
-        const int bk = b_koff(k, u_c0 + lane_c, u_ks, u_kr);
-        SDX_DCHECK(!ok || (long)b_off[i] + bk + 8 <= p.b_elems);
-        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + bk) : zp;
+        SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
+        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -611,9 +730,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const bool ok = kok && b_off[i] >= 0;
-      const int bk = b_koff(k, kc, ks, kr);
-      SDX_DCHECK(!ok || (long)b_off[i] + bk + 8 <= p.b_elems);
-      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + bk) : zp;
+      SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
+      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                        16, 0, 0);
@@ -1020,6 +1138,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
     __syncthreads();   // C-tile reads of the store loop are done
     float* red = reinterpret_cast<float*>(smem);   // [NT/64][3][BN]
     static_assert((NT / 64) * 3 * BN * 4 <= LDS, "BN-bwd stat reduction must fit the staging LDS");
+    static_assert(!SF || 16 + (NT / BN) * 3 * BN * 8 <= LDS, "StatFuse tail scratch must fit the staging LDS");
     if (lane < CPR) {
 #pragma unroll
       for (int k = 0; k < 3; ++k)
@@ -1032,7 +1151,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       float s = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < NT / 64; ++w2) s += red[(w2 * 3 + k) * BN + col];
-      if (n0 + col < p.Ncol) p.bs.slab[((size_t)(p.bs.row0 + mt) * bs_ns + k) * p.Ncol + n0 + col] = s;
+      if (n0 + col < p.Ncol) {
+        float* dst = p.bs.slab + ((size_t)(p.bs.row0 + mt) * bs_ns + k) * p.Ncol + n0 + col;
+        if constexpr (SF) st_sc1(dst, s);
+        else *dst = s;
+      }
+    }
+    if constexpr (SF) {
+      if (bs_ns == 3) stat_fuse_tail<NT, BN, 3>(p.sf, p.bs.slab, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
+      else stat_fuse_tail<NT, BN, 2>(p.sf, p.bs.slab, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
     }
   }
 
@@ -1072,8 +1199,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(IgemmParams p) {
       float s = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < WM; ++w2) s += red[(w2 * 2 + which) * BN + col];
-      if (n0 + col < p.Ncol) p.stats[((size_t)mt * 2 + which) * p.Ncol + n0 + col] = s;
+      if (n0 + col < p.Ncol) {
+        float* dst = p.stats + ((size_t)mt * 2 + which) * p.Ncol + n0 + col;
+        if constexpr (SF) st_sc1(dst, s);
+        else *dst = s;
+      }
     }
+    if constexpr (SF) stat_fuse_tail<NT, BN, 2>(p.sf, p.stats, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
   }
 }
 
@@ -1179,6 +1311,20 @@ hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
     }
     return hipErrorInvalidValue;
   }
+  if (p.sf.cnt != nullptr) {
+    // in-kernel statistics reduction: LDS-DMA variants only (launch_cfg routes here)
+    if constexpr (DEPTH == 3 && MODE != MODE_WGRAD) {
+      constexpr int V = MODE == MODE_DGRAD ? 3 : 1;
+      if (MODE == MODE_DGRAD && !bs) return hipErrorInvalidValue;
+      if (p.Kdim <= BK && igemm_one())
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, V, true>), g, b, 0, s, p);
+      else
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, V, false>), g, b, 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+    return hipErrorInvalidValue;
+  }
   if constexpr (DEPTH == 3 && MODE != MODE_WGRAD) {
     if (p.Kdim <= BK && igemm_one()) {
       if (MODE == MODE_DGRAD && bs)
@@ -1223,6 +1369,9 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   p.m_tiles = (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
   const int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
+  if (p.sf.cnt != nullptr &&
+      (MODE == MODE_WGRAD || p.sf.group < 1 || p.sf.n_groups != (p.m_tiles + p.sf.group - 1) / p.sf.group))
+    return hipErrorInvalidValue;   // the plan must match this tile config (stat_fuse_groups)
   if constexpr (MODE == MODE_WGRAD) {
     const ConvGeom& g = p.g;
     const bool k1 = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
@@ -1237,6 +1386,10 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   {
     // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
     // (SDX_IGEMM_GLDS=2 enables it there too)
+    if (p.sf.cnt != nullptr) {
+      if (p.in_scale != nullptr) return hipErrorInvalidValue;
+      return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
+    }
     if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
       if constexpr (MODE != MODE_WGRAD) {
         if (igemm_ring() && p.Kdim > 2 * BK) return launch_k<MODE, BM, BN, WM, WN, 4>(bs, grid, p, s);
@@ -1292,9 +1445,14 @@ void set_epi(IgemmParams& p, const GemmEpi* epi) {
 }  // namespace
 
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
-                           hipStream_t s, const float* in_scale, const float* in_shift, const GemmEpi* epi) {
+                           hipStream_t s, const float* in_scale, const float* in_shift, const GemmEpi* epi,
+                           const StatFuse* sf) {
   IgemmParams p{};
   set_epi(p, epi);
+  if (sf != nullptr) {
+    if (stats == nullptr) return hipErrorInvalidValue;
+    p.sf = *sf;
+  }
   if (p.out_f32 && stats != nullptr) return hipErrorInvalidValue;
   p.in_scale = in_scale;
   p.in_shift = in_shift;
@@ -1330,9 +1488,14 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
-                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi, int wt_full) {
+                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi,
+                                   const StatFuse* sf) {
   IgemmParams p{};
-  p.b_rsk = (wt_full && g.stride > 1) ? g.R * g.S * g.K : 0;
+  if (sf != nullptr) {
+    // a single-launch dgrad only (a strided dgrad's classes fill one slab in several launches)
+    if (bstat == nullptr || bstat->slab == nullptr || g.stride != 1 || bstat->row0 != 0) return hipErrorInvalidValue;
+    p.sf = *sf;
+  }
   set_epi(p, epi);
   if (p.out_f32 && (g.stride != 1 || addend != nullptr || (bstat != nullptr && bstat->slab != nullptr)))
     return hipErrorInvalidValue;
@@ -1352,8 +1515,19 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   p.Ncol = g.C;
   p.Kdim = p.nr * p.ns * g.K;
   p.a_elems = (long)g.N * g.P * g.Q * g.K;
-  p.b_elems = (long)p.Ncol * (p.b_rsk > 0 ? p.b_rsk : p.Kdim);
+  p.b_elems = (long)p.Ncol * p.Kdim;
   return launch_any<MODE_DGRAD>(p, cfg, s);
+}
+
+int stat_fuse_groups(int m_tiles) {
+  int g = 1;
+  while (g * g < m_tiles) ++g;   // ~sqrt: level-1 and level-2 reductions of similar length
+  return g;
+}
+
+int stat_fuse_counters(int m_tiles, int n_tiles) {
+  const int g = stat_fuse_groups(m_tiles);
+  return ((m_tiles + g - 1) / g + 1) * n_tiles;
 }
 
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits) {

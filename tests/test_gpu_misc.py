@@ -188,3 +188,46 @@ def test_cuda_graph_follows_eager_trajectory(gpu, tmp_path):
     rel = float((w0 - w1).norm() / (w0 - i0).norm())
     assert rel < 2e-2, rel
     assert torch.allclose(r0, r1, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_stat_fuse_matches_column_reduce(gpu, name):
+    """In-kernel BN-statistics reduction (StatFuse: the conv's last block reduces the slab and
+    finalizes the BN / evaluates the backward coefficients) == the separate column-reduce
+    launches, and is run-to-run deterministic."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    m = _ext.require()
+    torch.manual_seed(0)
+    base = SupConResNet(name).to(gpu).to(memory_format=torch.channels_last)
+    x = to_nhwc_input(torch.randn(32, 3, 32, 32, device=gpu))
+    w = torch.randn(32, 128, device=gpu)
+
+    def run(fuse):
+        prev = m.stat_fuse_set(3 if fuse else 0)
+        try:
+            net = SupConResNet(name).to(gpu).to(memory_format=torch.channels_last)
+            net.load_state_dict(base.state_dict())
+            f = FlatParams(net)
+            r = ModelRunner(net, "native", master=f.flat, fused=True)
+            f.zero_grad()
+            out = r.forward(x)
+            (out * w).sum().backward()
+            torch.cuda.synchronize()
+            bn = net.encoder.layer1[0].bn1
+            return out.detach().float(), f.grad.clone(), bn.running_mean.clone(), bn.running_var.clone()
+        finally:
+            m.stat_fuse_set(prev)
+
+    o1, g1, rm1, rv1 = run(True)
+    o2, g2, rm2, rv2 = run(True)
+    assert torch.equal(o1, o2) and torch.equal(g1, g2), "StatFuse must be deterministic"
+    o0, g0, rm0, rv0 = run(False)
+    torch.testing.assert_close(rm1, rm0, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(rv1, rv0, rtol=1e-6, atol=1e-7)
+    assert ((o1 - o0).norm() / o0.norm()).item() < 1e-3
+    # fp64 sums in another order: last-bit flips of the fp32 coefficients, compounded
+    # through bf16 roundings block by block (same envelope as the dgrad-epilogue statistics)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2

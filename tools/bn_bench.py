@@ -35,6 +35,7 @@ def main():
         out = m.bn_apply(y, sc, sh, None, None, None, 0, True)
         ca = m.bn_bwd_coef(m.bn_bwd_reduce(d, out, y, mu), float(N * H * H), sc, mu, iv)[0]
         cases = {
+            "copy(torch)": (lambda: y.clone(), 2),
             "apply(relu)": (lambda: m.bn_apply(y, sc, sh, None, None, None, 0, True), 2),
             "apply(+res)": (lambda: m.bn_apply(y, sc, sh, r, None, None, 2, True), 3),
             "bwd_reduce(out)": (lambda: m.bn_bwd_reduce(d, out, y, mu), 3),
