@@ -5,17 +5,20 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
+# NPROC (default 2): ranks to start (<= 16 on one box); PORT: rendezvous port
+NP=${NPROC:-2}
+PORT=${PORT:-29561}
 O=gpurun_out/multirank
 mkdir -p $O
 run() {  # $1 = tag, rest = extra bench args
-  tag=$1; shift
-  timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29561 bench.py --gpus 2 --steps 10 --warmup 3 "$@" > $O/$tag.log 2>&1
+  tag=$1_np$NP; shift
+  timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP --master-addr 127.0.0.1 \
+    --master-port $PORT bench.py --gpus $NP --steps 10 --warmup 3 "$@" > $O/$tag.log 2>&1
 }
 run nccl; rc=$?
-echo "nccl rc=$rc"; grep '"metric"' $O/nccl.log || tail -15 $O/nccl.log
+echo "nccl rc=$rc"; grep '"metric"' $O/nccl_np$NP.log || tail -15 $O/nccl_np$NP.log
 [ $rc -eq 0 ] && exit 0
 [ $rc -ne 1 ] && exit $rc
 run gloo --dist_backend gloo; rc=$?
-echo "gloo rc=$rc"; grep '"metric"' $O/gloo.log || tail -15 $O/gloo.log
+echo "gloo rc=$rc"; grep '"metric"' $O/gloo_np$NP.log || tail -15 $O/gloo_np$NP.log
 exit $rc
