@@ -351,6 +351,14 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
               "wgrad geometry mismatch");
   c10::DeviceGuard dg(x.device());
   const int64_t M = g.K, Ncol = (int64_t)R * S * g.C, Kd = (int64_t)g.N * g.P * g.Q;
+  // cfg 9 = the tap-reuse 3x3 kernel (wgrad3x3.hip), which auto (cfg -1) picks for every
+  // shape it supports (SDX_WGRAD3=0: generic implicit GEMM only); cfg -2 = generic auto
+  static const bool w3_on = [] {
+    const char* e = getenv("SDX_WGRAD3");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const bool w3 = (cfg == 9 || (cfg == -1 && w3_on && splits <= 0)) && !in_scale.has_value() && wgrad3x3_supported(g);
+  TORCH_CHECK(cfg != 9 || w3, "conv_wgrad: cfg 9 needs a stride-1 pad-1 3x3 conv with W in {4,8,16,32}, C,K % 64 == 0");
   // 64-output-channel GEMMs with a wide reduction side (layer-1 3x3: 64 x 576): the 64x256
   // tile (four 64x64 wave tiles) beats the exact-fit 64x64 one despite its padding, at
   // ~512 blocks (tools/wgrad_split_probe.py: 145 -> 124 us)
@@ -358,23 +366,42 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     const char* e = getenv("SDX_WGRAD_WIDE64");
     return e == nullptr || atoi(e) != 0;
   }();
-  if (wide64 && cfg < 0 && splits <= 0 && M <= 64 && Ncol >= 512) cfg = 2;
-  if (cfg < 0) cfg = auto_cfg(M, Ncol);
-  if (splits <= 0) {
-    const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
-                          ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
-    splits = std::max<int64_t>(1, 512 / tiles);
-    const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
-    splits = std::min(splits, max_splits);
-    // bound the fp32 partial slab to ~64 MiB, and to ~16 MiB / 256 splits for 1x1 GEMMs with
-    // a small output (M*Ncol <= 64K: the layer-1/2 pointwise convs), where the slab round
-    // trip outweighs the extra splits' parallelism (profiles/wgrad_sweep_r1.txt: 83 -> 67 us
-    // on the 256x64 layer-1 GEMMs; the 3x3 and larger GEMMs keep more splits)
-    const bool small_1x1 = R == 1 && S == 1 && M * Ncol <= 65536;
-    splits = std::min<int64_t>(splits, std::max<int64_t>(1, (small_1x1 ? (4LL << 20) : (16LL << 20)) / (M * Ncol)));
-    if (small_1x1) splits = std::min<int64_t>(splits, 256);
+  if (w3) {
+    if (splits <= 0) {
+      // SDX_W3_BLOCKS (default 256) blocks = ONE wave of 8-wave blocks over the 256 CUs (the
+      // kernel holds one block per CU); >= 8 steps per split. tools/w3_sweep.py: 256 blocks
+      // beats 128 (half the CUs idle) and 512 (a second partial round + twice the fp32
+      // partial slab) on every CIFAR 3x3 shape by 1.2-2.7x
+      static const int64_t target = [] {
+        const char* e = getenv("SDX_W3_BLOCKS");
+        return e ? atoll(e) : 256LL;
+      }();
+      const int64_t tiles = wgrad3x3_tiles(g), steps = wgrad3x3_steps(g);
+      splits = std::max<int64_t>(1, target / tiles);
+      splits = std::min(splits, std::max<int64_t>(1, steps / 8));
+    }
+    const int64_t steps = wgrad3x3_steps(g);
+    const int64_t per = (steps + splits - 1) / splits;
+    splits = (steps + per - 1) / per;
+  } else {
+    if (wide64 && cfg < 0 && splits <= 0 && M <= 64 && Ncol >= 512) cfg = 2;
+    if (cfg < 0) cfg = auto_cfg(M, Ncol);
+    if (splits <= 0) {
+      const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
+                            ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
+      splits = std::max<int64_t>(1, 512 / tiles);
+      const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
+      splits = std::min(splits, max_splits);
+      // bound the fp32 partial slab to ~64 MiB, and to ~16 MiB / 256 splits for 1x1 GEMMs with
+      // a small output (M*Ncol <= 64K: the layer-1/2 pointwise convs), where the slab round
+      // trip outweighs the extra splits' parallelism (profiles/wgrad_sweep_r1.txt: 83 -> 67 us
+      // on the 256x64 layer-1 GEMMs; the 3x3 and larger GEMMs keep more splits)
+      const bool small_1x1 = R == 1 && S == 1 && M * Ncol <= 65536;
+      splits = std::min<int64_t>(splits, std::max<int64_t>(1, (small_1x1 ? (4LL << 20) : (16LL << 20)) / (M * Ncol)));
+      if (small_1x1) splits = std::min<int64_t>(splits, 256);
+    }
+    splits = conv_wgrad_splits(g, (int)cfg, (int)splits);
   }
-  splits = conv_wgrad_splits(g, (int)cfg, (int)splits);
   torch::Tensor dw;
   if (out.has_value()) {
     dw = *out;
@@ -392,6 +419,12 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   torch::Tensor part;
   if (splits > 1 || accumulate)
     part = torch::empty({splits * M * Ncol}, x.options().dtype(at::kFloat));
+  if (w3) {
+    check_hip(launch_wgrad3x3(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
+                              dw.data_ptr<float>(), (int)splits, accumulate ? 1 : 0, cur_stream()),
+              "conv_wgrad(3x3)");
+    return dw;
+  }
   check_hip(launch_conv_wgrad(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
                               dw.data_ptr<float>(), (int)cfg, (int)splits, accumulate ? 1 : 0, cur_stream(), isc, ish),
             "conv_wgrad");

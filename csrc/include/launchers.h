@@ -85,6 +85,15 @@ int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
 hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int cfg,
                              int splits, int accumulate, hipStream_t s, const float* in_scale = nullptr,
                              const float* in_shift = nullptr);
+// dW (+)= Σ_split partial[split] (fp32 [splits][n4*4]), deterministic order
+hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float* dw, int accumulate, hipStream_t s);
+// Tap-reuse 3x3 wgrad (wgrad3x3.hip): stride 1, pad 1, W in {4,8,16,32}, C,K % 64 == 0.
+// partial: fp32 [splits][K][9C] (unused when splits == 1 and !accumulate)
+bool wgrad3x3_supported(const ConvGeom& g);
+int wgrad3x3_tiles(const ConvGeom& g);
+int wgrad3x3_steps(const ConvGeom& g);
+hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
+                           int accumulate, hipStream_t s);
 
 // ---- BatchNorm (bn.hip) ---------------------------------------------------------
 // Per-channel finalize (forward) and coefficient (backward) arguments, evaluated either by

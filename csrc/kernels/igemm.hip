@@ -1573,9 +1573,12 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
   p.out = direct ? (void*)dw : (void*)partial;
   hipError_t e = launch_any<MODE_WGRAD>(p, cfg, s);
   if (e != hipSuccess || direct) return e;
-  const long n4 = (long)p.M * p.Ncol / 4;
+  return launch_splitk_reduce(partial, p.splits, (long)p.M * p.Ncol / 4, dw, accumulate, s);
+}
+
+hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float* dw, int accumulate, hipStream_t s) {
   const long grid = (n4 + 63) / 64;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, partial, p.splits, n4, dw, accumulate);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, partial, splits, n4, dw, accumulate);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -1,0 +1,285 @@
+// Tap-reuse 3x3 weight gradient (stride 1, pad 1) on gfx950 MFMA, NHWC bf16 -> fp32.
+//
+//   dW[k][r][s][c] = Σ_{n,h,w} dy[n][h][w][k] · x[n][h+r−1][w+s−1][c]
+//
+// The generic implicit-GEMM wgrad (igemm.hip, MODE_WGRAD) treats the 9 taps as 9 separate
+// column tiles, so every tap tile re-reads the dy tile and its own shifted copy of x. Here
+// one 512-thread block owns 64 output channels × 64 input channels × ALL 9 taps (576 GEMM
+// columns) and walks its K-split 32 pixels at a time: per step it stages the 32×64 dy tile
+// and a zero-padded window of x — the 3 source rows (h−1, h, h+1) of every image row of
+// the step, one zero column on each side — ONCE in LDS, and the 9 taps read that window at
+// row/column offsets (r, s). Operand traffic per MFMA is ~2.3x lower than the tap-tiled GEMM.
+//
+// Shapes: square images of width W ∈ {4, 8, 16, 32} (a 32-pixel step is 32/W whole image rows, which
+// may span several images; each row's source rows are validated against its own image),
+// C % 64 == 0, K % 64 == 0 — every 3x3 conv of the CIFAR ResNets (reference
+// networks/resnet_big.py:41-47, conv2 of each Bottleneck / both convs of a BasicBlock).
+// Other shapes use the generic kernel.
+//
+// LDS rows are 64 bf16 (128 B); the 16-B chunk index is XOR-swizzled by g(R) = (R/2 + 2·(R/8))
+// mod 4 (in 32-B blocks). A ds_read_b64_tr_b16 half-wave reads 8 rows x 32 B: rows R0+{0..3}
+// and R0+{8..11} (+16k) for consecutive pixels, and this swizzle puts them on distinct banks
+// for ANY R0 — i.e. for every tap shift. Multi-row steps keep that pattern by padding the
+// window row pitch to P ≡ 8 (mod 16) rows between pixel rows 8 apart (W=8: P=24, W=4: P=12;
+// W=16/32 read within one row). Fragments follow igemm.hip's convention: the MFMA is issued
+// as D = Bᵀ·Aᵀ, so each lane holds 4 consecutive output columns of one output row. Output:
+// an fp32 partial slab per K-split, reduced deterministically by the split-K reduction of
+// igemm.hip (no atomics).
+#include <type_traits>
+
+#include "common.h"
+#include "launchers.h"
+
+using namespace sdx;
+
+namespace {
+
+constexpr int W3_NT = 512;      // 8 waves: 2 (output channels) x 4 (columns)
+constexpr int W3_ROWB = 128;    // LDS row: 64 bf16
+constexpr int W3_DY_BYTES = 32 * W3_ROWB;
+constexpr int W3_PF = 4;        // steps of loads in flight (register ring of 4 named slots)
+
+typedef __attribute__((address_space(3))) bf16x4 w3_lds_bf16x4;
+
+__device__ __attribute__((aligned(16))) uint16_t w3_zero16[8];
+
+// byte offset of 16-B chunk ch of LDS row R
+__device__ __forceinline__ int w3_off(int R, int ch) {
+  const int g = ((R >> 1) + 2 * (R >> 3)) & 3;
+  return R * W3_ROWB + ((ch ^ (g << 1)) << 4);
+}
+
+struct W3Params {
+  const uint16_t* dy;   // [N*H*W][K]
+  const uint16_t* x;    // [N*H*W][C]
+  float* part;          // [splits][K][9*C]
+  int K, C;
+  int steps_total;      // N*H*W / 32
+  int steps_per_split;
+  int k_tiles, c_tiles, splits;
+};
+
+template <int W>
+struct W3Geom {
+  static constexpr int RPS = 32 / W;                                   // image rows per step
+  static constexpr int P = W == 32 ? 34 : W == 16 ? 18 : W == 8 ? 24 : 12;   // window row pitch
+  static_assert(P >= W + 2, "pad columns");
+  static constexpr int XROWS = 3 * RPS * P;                            // LDS rows of the x window
+  static constexpr int STAGE = W3_DY_BYTES + XROWS * W3_ROWB;
+};
+
+template <int W>
+__global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
+  using G = W3Geom<W>;
+  constexpr int RPS = G::RPS;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h4 = lane >> 4, c16 = lane & 15;
+  const int wm = wv >> 2, wn = wv & 3;
+
+  // ---- tile / split (split-major: an XCD's co-resident blocks share one pixel range) ----
+  const int tiles = p.k_tiles * p.c_tiles;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lin % tiles, split = lin / tiles;
+  const int k0 = (tile / p.c_tiles) * 64, c0 = (tile % p.c_tiles) * 64;
+  const int s_begin = split * p.steps_per_split;
+  const int s_end = min(p.steps_total, s_begin + p.steps_per_split);
+
+  // ---- zero the pad columns of both x windows (never written by the loads) ----
+  for (int e = tid; e < 2 * 3 * RPS * 2 * 8; e += W3_NT) {
+    const int ch = e & 7, side = (e >> 3) & 1, ri = (e >> 4) % (3 * RPS), buf = (e >> 4) / (3 * RPS);
+    const int row = ri * G::P + (side ? W + 1 : 0);
+    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + W3_DY_BYTES + w3_off(row, ch)) = make_uint4(0u, 0u, 0u, 0u);
+  }
+
+  // ---- loader: 1024 16-B chunks per step, 2 per thread: chunk tid is a dy chunk for the
+  // first 256 threads and an x-window chunk otherwise; chunk tid + 512 is always x ----
+  // x-window chunk e (0..767): channel chunk e%8 of pixel w of window row ri = (r, i)
+  // steps at or past s_end (the unrolled loop's tail) load the zero page: they add nothing
+  auto x_src = [&](int e, int step) -> const uint16_t* {
+    const int ch = e & 7, rest = e >> 3;
+    const int w = rest % W, ri = rest / W;
+    const int r = ri / RPS, i = ri % RPS;
+    const int gr = step * RPS + i;                      // global image row (n*H + h), H == W
+    const int hs = (gr & (W - 1)) + r - 1;
+    const bool ok = step < s_end && (unsigned)hs < (unsigned)W;
+    return ok ? p.x + ((size_t)(gr + r - 1) * W + w) * p.C + c0 + ch * 8 : w3_zero16;
+  };
+  auto x_dst = [&](int e) -> int {
+    const int ch = e & 7, rest = e >> 3;
+    return W3_DY_BYTES + w3_off((rest / W) * G::P + rest % W + 1, ch);
+  };
+  const bool first_dy = tid < 256;
+  const int e0 = tid - 256, e1 = tid + 256;          // x chunk indices of chunks tid, tid + 512
+  const int dst0 = first_dy ? w3_off(tid >> 3, tid & 7) : x_dst(e0);
+  const int dst1 = x_dst(e1);
+  // register ring of 4 prefetched steps: slot u holds the step ≡ s_begin + u (mod 4). Named
+  // registers selected at compile time (an array indexed inside the lambdas goes to scratch)
+  uint4 ra0, rb0, ra1, rb1, ra2, rb2, ra3, rb3;
+  auto slot_a = [&](auto U) -> uint4& {
+    if constexpr (decltype(U)::value == 0) return ra0;
+    else if constexpr (decltype(U)::value == 1) return ra1;
+    else if constexpr (decltype(U)::value == 2) return ra2;
+    else return ra3;
+  };
+  auto slot_b = [&](auto U) -> uint4& {
+    if constexpr (decltype(U)::value == 0) return rb0;
+    else if constexpr (decltype(U)::value == 1) return rb1;
+    else if constexpr (decltype(U)::value == 2) return rb2;
+    else return rb3;
+  };
+  auto load = [&](int step, uint4& a, uint4& b) {
+    const uint16_t* s0 = first_dy ? (step < s_end ? p.dy + ((size_t)step * 32 + (tid >> 3)) * p.K + k0 + (tid & 7) * 8
+                                                   : w3_zero16)
+                                  : x_src(e0, step);
+    a = *reinterpret_cast<const uint4*>(s0);
+    b = *reinterpret_cast<const uint4*>(x_src(e1, step));
+  };
+  auto store = [&](int buf, const uint4& a, const uint4& b) {
+    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + dst0) = a;
+    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + dst1) = b;
+  };
+
+  // ---- fragment addressing: lane (h4, c16 = 4q + pp) reads K rows (pixels) 8h4+q and +4,
+  // columns col0 + 4pp .. +3 (ds_read_b64_tr_b16 transposes across the 4 q-lanes). The byte
+  // offsets are step-invariant: computed once (2 A + 9 B fragments, lo/hi rows). ----
+  const int q = c16 >> 2, pp = c16 & 3;
+  const int p_lo = 8 * h4 + q, p_hi = p_lo + 4;
+  const int xb_lo = (p_lo / W) * G::P + (p_lo % W);   // x-window row of pixel p, tap (0, 0)
+  const int xb_hi = (p_hi / W) * G::P + (p_hi % W);
+  auto lane_off = [&](int row, int col0) {
+    const int col = col0 + 4 * pp;
+    return w3_off(row, col >> 3) + (col & 7) * 2;
+  };
+  int ao_lo[2], ao_hi[2], bo_lo[9], bo_hi[9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    ao_lo[i] = lane_off(p_lo, wm * 32 + 16 * i);
+    ao_hi[i] = lane_off(p_hi, wm * 32 + 16 * i);
+  }
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int n = wn * 144 + 16 * j;             // wave column tile: one tap, 16 channels
+    const int t = n >> 6, r = t / 3, s = t - 3 * r;
+    const int off = r * RPS * G::P + s;
+    bo_lo[j] = W3_DY_BYTES + lane_off(xb_lo + off, n & 63);
+    bo_hi[j] = W3_DY_BYTES + lane_off(xb_hi + off, n & 63);
+  }
+  auto frag = [&](const unsigned char* base, int o_lo, int o_hi) -> bf16x8 {
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_lo));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_hi));
+    bf16x8 v;
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    return v;
+  };
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const unsigned char* base = smem + buf * G::STAGE;
+    bf16x8 af[2], bfr[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) bfr[j] = frag(base, bo_lo[j], bo_hi[j]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = frag(base, ao_lo[i], ao_hi[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
+
+  // ---- K loop: two LDS buffers, one barrier per step. The loads of step k+1+W3_PF are
+  // issued as step k+1 leaves the ring for LDS, so W3_PF steps of loads are always in
+  // flight: one step's MFMAs (~300 cycles a wave) are far shorter than an HBM miss. The loop
+  // is unrolled by W3_PF (even) and runs whole groups, so ring slots and LDS parity are
+  // compile-time. ----
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  // step k = base + U of the unrolled loop: compute from LDS buffer U&1, move step k+1 from
+  // its ring slot into the other buffer, refill that slot with step k+1+4. Branch-free (the
+  // tail steps read zeros), so the compiler's vmcnt waits retire only the oldest step's loads
+  auto iter = [&](int base, auto U) {
+    constexpr int u = decltype(U)::value;
+    using N = std::integral_constant<int, (u + 1) % W3_PF>;
+    compute(u & 1);
+    store((u + 1) & 1, slot_a(N{}), slot_b(N{}));
+    load(base + u + 1 + W3_PF, slot_a(N{}), slot_b(N{}));
+    __syncthreads();
+  };
+  load(s_begin, ra0, rb0);
+  load(s_begin + 1, ra1, rb1);
+  load(s_begin + 2, ra2, rb2);
+  load(s_begin + 3, ra3, rb3);
+  store(0, ra0, rb0);
+  load(s_begin + W3_PF, ra0, rb0);
+  __syncthreads();
+  for (int base = s_begin; base < s_end; base += W3_PF) {
+    iter(base, I0{});
+    iter(base, I1{});
+    iter(base, I2{});
+    iter(base, I3{});
+  }
+
+  // ---- epilogue: fp32 partial rows, 4 consecutive columns (same tap) per lane ----
+  const int Ncol = 9 * p.C;
+  float* out = p.part + (size_t)split * p.K * Ncol;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = k0 + wm * 32 + 16 * i + c16;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int n = wn * 144 + 16 * j + 4 * h4;
+      const int t = n >> 6;
+      *reinterpret_cast<float4*>(out + (size_t)m * Ncol + t * p.C + c0 + (n & 63)) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+}
+
+}  // namespace
+
+bool wgrad3x3_supported(const ConvGeom& g) {
+  const bool w_ok = g.W == 4 || g.W == 8 || g.W == 16 || g.W == 32;
+  return g.R == 3 && g.S == 3 && g.stride == 1 && g.pad == 1 && w_ok && g.H == g.W && g.P == g.H && g.Q == g.W &&
+         g.C % 64 == 0 && g.K % 64 == 0 && ((long)g.N * g.H * g.W) % 32 == 0;
+}
+
+int wgrad3x3_tiles(const ConvGeom& g) { return (g.K / 64) * (g.C / 64); }
+
+int wgrad3x3_steps(const ConvGeom& g) { return (int)((long)g.N * g.H * g.W / 32); }
+
+hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
+                           int accumulate, hipStream_t s) {
+  if (!wgrad3x3_supported(g) || splits < 1) return hipErrorInvalidValue;
+  W3Params p{};
+  p.dy = (const uint16_t*)dy;
+  p.x = (const uint16_t*)x;
+  p.K = g.K;
+  p.C = g.C;
+  p.steps_total = wgrad3x3_steps(g);
+  p.steps_per_split = (p.steps_total + splits - 1) / splits;
+  p.splits = (p.steps_total + p.steps_per_split - 1) / p.steps_per_split;
+  p.k_tiles = g.K / 64;
+  p.c_tiles = g.C / 64;
+  // one split straight into dW (unless accumulating into it)
+  const bool direct = p.splits == 1 && !accumulate;
+  if (!direct && partial == nullptr) return hipErrorInvalidValue;
+  p.part = direct ? dw : partial;
+  const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W3_NT);
+  switch (g.W) {
+    case 4: hipLaunchKernelGGL(wgrad3x3_kernel<4>, grid, block, 0, s, p); break;
+    case 8: hipLaunchKernelGGL(wgrad3x3_kernel<8>, grid, block, 0, s, p); break;
+    case 16: hipLaunchKernelGGL(wgrad3x3_kernel<16>, grid, block, 0, s, p); break;
+    default: hipLaunchKernelGGL(wgrad3x3_kernel<32>, grid, block, 0, s, p); break;
+  }
+  SDX_LAUNCH_CHECK();
+  if (direct) return hipSuccess;
+  return launch_splitk_reduce(partial, p.splits, (long)g.K * 9 * g.C / 4, dw, accumulate, s);
+}

@@ -81,6 +81,32 @@ def test_conv_wgrad(gpu, shape, cfg):
         assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
 
 
+@pytest.mark.parametrize("shape", [(4, 32, 32, 64, 64), (3, 16, 16, 128, 64), (2, 16, 16, 64, 128),
+                                   (5, 8, 8, 128, 128), (6, 4, 4, 64, 192), (4, 4, 4, 256, 64)])
+@pytest.mark.parametrize("splits", [1, 3, 0])
+def test_wgrad3x3_tap_reuse(gpu, shape, splits):
+    """Tap-reuse 3x3 wgrad (cfg 9, wgrad3x3.hip) vs fp32 torch: images of width 32/16/8/4
+    (a 32-pixel step spans 1/2/4/8 rows, crossing image boundaries at width 4 and 8),
+    direct (1 split), split-K, and auto split; plus accumulation into a KRSC sink."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, C, K = shape[0], shape[1], shape[3], shape[4]
+    x, w = _mk(N, H, H, C, K, 3)
+    wf = w.float().requires_grad_(True)
+    out = F.conv2d(x.float(), wf, padding=1)
+    dy = torch.randn_like(out).bfloat16()
+    (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
+    dyh, xh = dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    dw = m.conv_wgrad(dyh, xh, 3, 3, 1, 1, splits, 9)
+    assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
+    sink = torch.full((K, 3, 3, C), 0.25, device=gpu)
+    m.conv_wgrad(dyh, xh, 3, 3, 1, 1, splits, 9, sink, True)
+    assert _rel(sink - 0.25, dw.float()) < 1e-5
+    # auto dispatch picks the same kernel for these shapes
+    dw2 = m.conv_wgrad(dyh, xh, 3, 3, 1, 1, splits, -1) if splits == 0 else dw
+    assert torch.equal(dw2, dw)
+
+
 def test_conv_large_m(gpu):
     """Layer-1 scale (M = 512·32·32) against torch bf16 conv."""
     from simclr_pytorch_distributed_amd.ops import _ext
