@@ -95,15 +95,25 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   // ---- loader: 1024 16-B chunks per step, 2 per thread: chunk tid is a dy chunk for the
   // first 256 threads and an x-window chunk otherwise; chunk tid + 512 is always x ----
   // x-window chunk e (0..767): channel chunk e%8 of pixel w of window row ri = (r, i)
-  // steps at or past s_end (the unrolled loop's tail) load the zero page: they add nothing
-  auto x_src = [&](int e, int step) -> const uint16_t* {
+  // Per-thread loader state, fixed for the whole K loop: a step moves every chunk by 32
+  // pixels (dy: 32 rows of K; x: RPS image rows of W pixels = 32 pixels of C), so a load is
+  // base + step·stride plus, for x, the validity of its source row. Steps at or past s_end
+  // (the unrolled loop's tail) load the zero page: they add nothing.
+  // x-window chunk e (0..767): channel chunk e%8 of pixel w of window row ri = (r, i)
+  struct XChunk {
+    const uint16_t* base;   // x element of step 0 (may lie outside x: used only when valid)
+    int i, r;               // window image row within the step, tap row
+  };
+  auto x_chunk = [&](int e) -> XChunk {
     const int ch = e & 7, rest = e >> 3;
     const int w = rest % W, ri = rest / W;
     const int r = ri / RPS, i = ri % RPS;
-    const int gr = step * RPS + i;                      // global image row (n*H + h), H == W
-    const int hs = (gr & (W - 1)) + r - 1;
+    return {p.x + ((long)(i + r - 1) * W + w) * p.C + c0 + ch * 8, i, r};
+  };
+  auto x_src = [&](const XChunk& xc, int step) -> const uint16_t* {
+    const int hs = ((step * RPS + xc.i) & (W - 1)) + xc.r - 1;   // H == W
     const bool ok = step < s_end && (unsigned)hs < (unsigned)W;
-    return ok ? p.x + ((size_t)(gr + r - 1) * W + w) * p.C + c0 + ch * 8 : w3_zero16;
+    return ok ? xc.base + (long)step * 32 * p.C : w3_zero16;
   };
   auto x_dst = [&](int e) -> int {
     const int ch = e & 7, rest = e >> 3;
@@ -113,6 +123,8 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   const int e0 = tid - 256, e1 = tid + 256;          // x chunk indices of chunks tid, tid + 512
   const int dst0 = first_dy ? w3_off(tid >> 3, tid & 7) : x_dst(e0);
   const int dst1 = x_dst(e1);
+  const XChunk xc0 = x_chunk(first_dy ? 0 : e0), xc1 = x_chunk(e1);
+  const uint16_t* dy_base = p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
   // register ring of 4 prefetched steps: slot u holds the step ≡ s_begin + u (mod 4). Named
   // registers selected at compile time (an array indexed inside the lambdas goes to scratch)
   uint4 ra0, rb0, ra1, rb1, ra2, rb2, ra3, rb3;
@@ -129,11 +141,9 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
     else return rb3;
   };
   auto load = [&](int step, uint4& a, uint4& b) {
-    const uint16_t* s0 = first_dy ? (step < s_end ? p.dy + ((size_t)step * 32 + (tid >> 3)) * p.K + k0 + (tid & 7) * 8
-                                                   : w3_zero16)
-                                  : x_src(e0, step);
+    const uint16_t* s0 = first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : w3_zero16) : x_src(xc0, step);
     a = *reinterpret_cast<const uint4*>(s0);
-    b = *reinterpret_cast<const uint4*>(x_src(e1, step));
+    b = *reinterpret_cast<const uint4*>(x_src(xc1, step));
   };
   auto store = [&](int buf, const uint4& a, const uint4& b) {
     *reinterpret_cast<uint4*>(smem + buf * G::STAGE + dst0) = a;
@@ -168,10 +178,7 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   auto frag = [&](const unsigned char* base, int o_lo, int o_hi) -> bf16x8 {
     const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_lo));
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_hi));
-    bf16x8 v;
-    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    return v;
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
   f32x4 acc[2][9];
