@@ -359,6 +359,14 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   }();
   const bool w3 = (cfg == 9 || (cfg == -1 && w3_on && splits <= 0)) && !in_scale.has_value() && wgrad3x3_supported(g);
   TORCH_CHECK(cfg != 9 || w3, "conv_wgrad: cfg 9 needs a stride-1 pad-1 3x3 conv with W in {4,8,16,32}, C,K % 64 == 0");
+  // cfg 10 = the stride-1 1x1 kernel (wgrad1x1.hip), auto-picked for every shape it supports
+  // (SDX_WGRAD1=0: generic only)
+  static const bool w1_on = [] {
+    const char* e = getenv("SDX_WGRAD1");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const bool w1 = (cfg == 10 || (cfg == -1 && w1_on && splits <= 0)) && !in_scale.has_value() && wgrad1x1_supported(g);
+  TORCH_CHECK(cfg != 10 || w1, "conv_wgrad: cfg 10 needs a stride-1 1x1 conv with K,C % 128 == 0");
   // 64-output-channel GEMMs with a wide reduction side (layer-1 3x3: 64 x 576): the 64x256
   // tile (four 64x64 wave tiles) beats the exact-fit 64x64 one despite its padding, at
   // ~512 blocks (tools/wgrad_split_probe.py: 145 -> 124 us)
@@ -366,7 +374,20 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     const char* e = getenv("SDX_WGRAD_WIDE64");
     return e == nullptr || atoi(e) != 0;
   }();
-  if (w3) {
+  if (w1) {
+    // as for the 3x3 kernel: one wave of SDX_W3_BLOCKS (256) 8-wave blocks, >= 8 steps each
+    const int64_t steps = wgrad1x1_steps(g);
+    if (splits <= 0) {
+      static const int64_t target = [] {
+        const char* e = getenv("SDX_W3_BLOCKS");
+        return e ? atoll(e) : 256LL;
+      }();
+      splits = std::max<int64_t>(1, target / wgrad1x1_tiles(g));
+      splits = std::min(splits, std::max<int64_t>(1, steps / 8));
+    }
+    const int64_t per = (steps + splits - 1) / splits;
+    splits = (steps + per - 1) / per;
+  } else if (w3) {
     if (splits <= 0) {
       // SDX_W3_BLOCKS (default 256) blocks = ONE wave of 8-wave blocks over the 256 CUs (the
       // kernel holds one block per CU); >= 8 steps per split. tools/w3_sweep.py: 256 blocks
@@ -419,6 +440,12 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   torch::Tensor part;
   if (splits > 1 || accumulate)
     part = torch::empty({splits * M * Ncol}, x.options().dtype(at::kFloat));
+  if (w1) {
+    check_hip(launch_wgrad1x1(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
+                              dw.data_ptr<float>(), (int)splits, accumulate ? 1 : 0, cur_stream()),
+              "conv_wgrad(1x1)");
+    return dw;
+  }
   if (w3) {
     check_hip(launch_wgrad3x3(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
                               dw.data_ptr<float>(), (int)splits, accumulate ? 1 : 0, cur_stream()),

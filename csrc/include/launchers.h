@@ -94,6 +94,13 @@ int wgrad3x3_tiles(const ConvGeom& g);
 int wgrad3x3_steps(const ConvGeom& g);
 hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s);
+// Stride-1 1x1 wgrad (wgrad1x1.hip): K % 128 == 0, C % 128 == 0, N*H*W % 32 == 0.
+// partial: fp32 [splits][K][C] (unused when splits == 1 and !accumulate)
+bool wgrad1x1_supported(const ConvGeom& g);
+int wgrad1x1_tiles(const ConvGeom& g);
+int wgrad1x1_steps(const ConvGeom& g);
+hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
+                           int accumulate, hipStream_t s);
 
 // ---- BatchNorm (bn.hip) ---------------------------------------------------------
 // Per-channel finalize (forward) and coefficient (backward) arguments, evaluated either by
