@@ -375,12 +375,12 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     return e == nullptr || atoi(e) != 0;
   }();
   if (w1) {
-    // as for the 3x3 kernel: one wave of SDX_W3_BLOCKS (256) 8-wave blocks, >= 8 steps each
+    // as for the 3x3 kernel: SDX_W3_BLOCKS (128) 8-wave blocks, >= 8 steps each
     const int64_t steps = wgrad1x1_steps(g);
     if (splits <= 0) {
       static const int64_t target = [] {
         const char* e = getenv("SDX_W3_BLOCKS");
-        return e ? atoll(e) : 256LL;
+        return e ? atoll(e) : 128LL;
       }();
       splits = std::max<int64_t>(1, target / wgrad1x1_tiles(g));
       splits = std::min(splits, std::max<int64_t>(1, steps / 8));
@@ -389,13 +389,15 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     splits = (steps + per - 1) / per;
   } else if (w3) {
     if (splits <= 0) {
-      // SDX_W3_BLOCKS (default 256) blocks = ONE wave of 8-wave blocks over the 256 CUs (the
-      // kernel holds one block per CU); >= 8 steps per split. tools/w3_sweep.py: 256 blocks
-      // beats 128 (half the CUs idle) and 512 (a second partial round + twice the fp32
-      // partial slab) on every CIFAR 3x3 shape by 1.2-2.7x
+      // SDX_W3_BLOCKS (default 128) 8-wave blocks, >= 8 steps per split. Standalone, 256
+      // blocks (one per CU) is fastest (tools/w3_sweep.py), but in the training step these
+      // kernels run on the wgrad side stream: a block holds ~416 of a SIMD lane's 512 VGPRs,
+      // so the critical-path kernels (128-VGPR dgrads, the BN reductions) cannot co-reside on
+      // its CU. 128 blocks leave half the CUs to the main stream: step 13.71 -> 13.34 ms at
+      // 256 images/GPU, 8.48 -> 8.20 ms at 128 (profiles/wgrad3x3_r2.txt)
       static const int64_t target = [] {
         const char* e = getenv("SDX_W3_BLOCKS");
-        return e ? atoll(e) : 256LL;
+        return e ? atoll(e) : 128LL;
       }();
       const int64_t tiles = wgrad3x3_tiles(g), steps = wgrad3x3_steps(g);
       splits = std::max<int64_t>(1, target / tiles);
@@ -410,7 +412,12 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     if (splits <= 0) {
       const int64_t tiles = ((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg)) *
                             ((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
-      splits = std::max<int64_t>(1, 512 / tiles);
+      // SDX_WGRAD_TARGET: block target of the generic wgrad split heuristic (default 512)
+      static const int64_t gen_target = [] {
+        const char* e = getenv("SDX_WGRAD_TARGET");
+        return e ? atoll(e) : 512LL;
+      }();
+      splits = std::max<int64_t>(1, gen_target / tiles);
       const int64_t max_splits = std::max<int64_t>(1, Kd / 512);   // >= 8 K-tiles per split
       splits = std::min(splits, max_splits);
       // bound the fp32 partial slab to ~64 MiB, and to ~16 MiB / 256 splits for 1x1 GEMMs with
