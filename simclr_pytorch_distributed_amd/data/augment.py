@@ -10,6 +10,7 @@ random draws, in torch (CPU runs, and the oracle the GPU kernel is tested agains
 from __future__ import annotations
 
 import math
+import dataclasses
 from dataclasses import dataclass
 from typing import Sequence
 
@@ -226,3 +227,34 @@ def augment(data: torch.Tensor, idx: torch.Tensor, cfg: AugConfig, seed: int, of
 def nhwc8_to_nchw(x: torch.Tensor) -> torch.Tensor:
     """NHWC [.., 8] -> NCHW float [.., 3, H, W] for the torch backend."""
     return x[..., :3].permute(0, 3, 1, 2).float().contiguous()
+
+
+class SimCLRAugment:
+    """Per-sample callable form of the SimCLR augmentation (reference main_supcon.py:170-179):
+    a uint8 HWC image tensor -> normalized float CHW [3, S, S], with the same draws as the
+    batched kernels. Each call advances an internal counter, so repeated calls on one image
+    give independent views (use with :class:`TwoCropTransform`)."""
+
+    def __init__(self, cfg: AugConfig, seed: int = 0):
+        self.cfg = dataclasses.replace(cfg, n_views=1)
+        self.seed = int(seed)
+        self._calls = 0
+
+    def __call__(self, img: torch.Tensor) -> torch.Tensor:
+        assert img.dtype == torch.uint8 and img.dim() == 3 and img.shape[2] == 3, "uint8 HWC image"
+        self._calls += 1
+        out = augment_reference(img.unsqueeze(0), torch.zeros(1, dtype=torch.long), self.cfg,
+                                _mix64((self.seed * 0x9E3779B97F4A7C15 + self._calls) & M64))
+        return out[0, :, :, :3].permute(2, 0, 1).contiguous()
+
+
+class TwoCropTransform:
+    """Two independently augmented views of one sample (reference util.py:10-16). The
+    training engines draw both views of a whole batch in one GPU launch instead
+    (:func:`gpu_augment` with ``n_views=2``); this wrapper serves per-sample pipelines."""
+
+    def __init__(self, transform):
+        self.transform = transform
+
+    def __call__(self, x):
+        return [self.transform(x), self.transform(x)]

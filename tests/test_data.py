@@ -63,3 +63,16 @@ def test_engine_step_image_folder_cpu_aug(tmp_path, gpu_aug):
     assert eng.data_offs is not None and eng.data.dim() == 1
     st = eng.train_step(torch.arange(4), 1, 0, 2)
     assert torch.isfinite(st["loss_local"])
+
+
+def test_two_crop_transform_gives_two_distinct_views():
+    """TwoCropTransform(SimCLRAugment) (reference util.py:10-16 with the SimCLR pipeline):
+    two normalized [3, S, S] views of one uint8 image, drawn independently."""
+    from simclr_pytorch_distributed_amd.data.augment import AugConfig, SimCLRAugment, TwoCropTransform
+    g = torch.Generator().manual_seed(0)
+    img = torch.randint(0, 256, (40, 40, 3), dtype=torch.uint8, generator=g)
+    t = TwoCropTransform(SimCLRAugment(AugConfig(size=32), seed=3))
+    v1, v2 = t(img)
+    assert v1.shape == v2.shape == (3, 32, 32) and v1.dtype == torch.float32
+    assert not torch.equal(v1, v2)
+    assert torch.isfinite(v1).all() and torch.isfinite(v2).all()
