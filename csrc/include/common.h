@@ -135,5 +135,19 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 
 }  // namespace sdx
 
+#ifndef SDX_NT_EW
+#define SDX_NT_EW 0   // 1: non-temporal 16-B stores in the elementwise BN kernels (A/B experiment)
+#endif
+// 16-B store of a streamed output that no kernel re-reads soon (non-temporal when enabled)
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  if constexpr (NT) {
+    typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(nt_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+
 #define SDX_LAUNCH_CHECK() \
   do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return e__; } while (0)

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     op.load(sc, sh, sc2, sh2, (e0 % C8) * 8);
     for (int e = e0; e < n8; e += stride) {
       const uint4 o = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
-      O[e] = o;
+      st16<SDX_NT_EW != 0>(O + e, o);
       if (mask_out) mask_out[e] = relu_bits(o);
     }
   } else {
@@ -407,9 +407,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
     float d[8];
     uint4 ra, rb;
     op.run(dv, ov, has_out, av, bv, d, ra, rb, omask, e);
-    if (DZ) DZ[e] = pack8(d);
-    DA[e] = ra;
-    if (TWO) DB[e] = rb;
+    if (DZ) st16<SDX_NT_EW != 0>(DZ + e, pack8(d));
+    st16<SDX_NT_EW != 0>(DA + e, ra);
+    if (TWO) st16<SDX_NT_EW != 0>(DB + e, rb);
   };
   if ((stride % C8) == 0) {
     op.load(ca, cb, msc, msh, C, (e0 % C8) * 8);

@@ -46,6 +46,12 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
+#ifndef SDX_NT_STORE
+// non-temporal stores of the bf16 conv outputs (they are re-read only by later kernels):
+// plain dgrad 2.69 -> 2.44 ms, fwd 2.53 -> 2.27 ms per step, step -2.5 % (same box,
+// profiles/nt_store_r2.txt); 0 restores write-back stores
+#define SDX_NT_STORE 1
+#endif
 
 struct IgemmParams {
   ConvGeom g;
@@ -1094,7 +1100,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
           }
           v = make_uint4(r[0], r[1], r[2], r[3]);
         }
-        *reinterpret_cast<uint4*>(out + o) = v;
+        st16<SDX_NT_STORE != 0>(out + o, v);
         if (MODE == MODE_DGRAD && bst) {
           // statistics of the stored (bf16-rounded) values, as bn_bwd_reduce would read them
           float d[8], ya[8];
