@@ -138,6 +138,25 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 #ifndef SDX_NT_EW
 #define SDX_NT_EW 0   // 1: non-temporal 16-B stores in the elementwise BN kernels (A/B experiment)
 #endif
+#ifndef SDX_NT_EW_LOAD
+// non-temporal loads of the elementwise BN kernels' read-once inputs: step 12.90 -> 12.77 ms
+// on the same box (profiles/nt_store_r2.txt); 0 = cached loads
+#define SDX_NT_EW_LOAD 1
+#endif
+#ifndef SDX_NT_PART
+#define SDX_NT_PART 0      // 1: non-temporal split-K partial slab stores + reduction loads (A/B)
+#endif
+// 16-B load of a read-once input (non-temporal when enabled)
+template <bool NT>
+__device__ __forceinline__ uint4 ld16s(const void* p) {
+  if constexpr (NT) {
+    typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
+    const nt_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(p));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
 // 16-B store of a streamed output that no kernel re-reads soon (non-temporal when enabled)
 template <bool NT>
 __device__ __forceinline__ void st16(void* p, uint4 v) {

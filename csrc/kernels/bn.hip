@@ -212,7 +212,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
   if ((stride % C8) == 0) {
     op.load(sc, sh, sc2, sh2, (e0 % C8) * 8);
     for (int e = e0; e < n8; e += stride) {
-      const uint4 o = op.run(Y[e], RES != 0 ? R[e] : make_uint4(0, 0, 0, 0));
+      const uint4 o = op.run(ld16s<SDX_NT_EW_LOAD != 0>(Y + e),
+                             RES != 0 ? ld16s<SDX_NT_EW_LOAD != 0>(R + e) : make_uint4(0, 0, 0, 0));
       st16<SDX_NT_EW != 0>(O + e, o);
       if (mask_out) mask_out[e] = relu_bits(o);
     }
@@ -413,7 +414,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   };
   if ((stride % C8) == 0) {
     op.load(ca, cb, msc, msh, C, (e0 % C8) * 8);
-    for (int e = e0; e < n8; e += stride) one(e, D[e], has_out ? OV[e] : z, YA[e], TWO ? YB[e] : z);
+    for (int e = e0; e < n8; e += stride)
+      one(e, ld16s<SDX_NT_EW_LOAD != 0>(D + e), has_out ? ld16s<SDX_NT_EW_LOAD != 0>(OV + e) : z,
+          ld16s<SDX_NT_EW_LOAD != 0>(YA + e), TWO ? ld16s<SDX_NT_EW_LOAD != 0>(YB + e) : z);
   } else {
     for (int e = e0; e < n8; e += stride) {
       op.load(ca, cb, msc, msh, C, (e % C8) * 8);

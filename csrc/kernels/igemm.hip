@@ -46,6 +46,11 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
+#ifndef SDX_NT_LOAD
+// non-temporal loads of the dgrad epilogue's read-once operands (addend, BN inputs): step
+// 13.15 -> 13.05 ms on the same box (profiles/nt_store_r2.txt); 0 = cached loads
+#define SDX_NT_LOAD 1
+#endif
 #ifndef SDX_NT_STORE
 // non-temporal stores of the bf16 conv outputs (they are re-read only by later kernels):
 // plain dgrad 2.69 -> 2.44 ms, fwd 2.53 -> 2.27 ms per step, step -2.5 % (same box,
@@ -336,6 +341,15 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   auto ld16_or_zero = [&](const uint16_t* q, bool ok) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(ok ? (gptr16)q : zp);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
+  // read-once epilogue operands (addend, BN input): optionally non-temporal
+  auto ld16_stream = [&](const uint16_t* q, bool ok) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const auto* ptr = (const __attribute__((address_space(1))) u32x4*)(ok ? (gptr16)q : zp);
+    u32x4 v;
+    if constexpr (SDX_NT_LOAD != 0) v = __builtin_nontemporal_load(ptr);
+    else v = *ptr;
     return make_uint4(v[0], v[1], v[2], v[3]);
   };
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -955,8 +969,10 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + wn * WTN + 16 * j + 4 * h;
         if (col < p.Ncol)
-          *reinterpret_cast<float4*>(out + (size_t)row * p.Ncol + col) =
-              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+          st16<SDX_NT_PART != 0 && MODE == MODE_WGRAD>(
+              out + (size_t)row * p.Ncol + col,
+              make_uint4(__float_as_uint(acc[i][j][0]), __float_as_uint(acc[i][j][1]), __float_as_uint(acc[i][j][2]),
+                         __float_as_uint(acc[i][j][3])));
       }
     }
     return;
@@ -1021,13 +1037,13 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       // (the zero page, not a private zero: a select between a global and a private
       // address would turn the load into a flat load and spill the zero to scratch)
       const int oa = ea[it];
-      pf_add[sl] = ld16_or_zero(p.addend + (oa >= 0 ? oa : 0), oa >= 0);
+      pf_add[sl] = ld16_stream(p.addend + (oa >= 0 ? oa : 0), oa >= 0);
       pf_am[sl] = (ok && p.addend_mask != nullptr) ? (uint32_t)p.addend_mask[o >> 3] : 0xffu;
     }
     if (MODE == MODE_DGRAD && bst) {
-      pf_ya[sl] = ld16_or_zero(reinterpret_cast<const uint16_t*>(p.bs.ya) + (ok ? o : 0), ok);
+      pf_ya[sl] = ld16_stream(reinterpret_cast<const uint16_t*>(p.bs.ya) + (ok ? o : 0), ok);
       const bool okb = ok && p.bs.yb != nullptr;
-      pf_yb[sl] = ld16_or_zero(reinterpret_cast<const uint16_t*>(p.bs.yb) + (okb ? o : 0), okb);
+      pf_yb[sl] = ld16_stream(reinterpret_cast<const uint16_t*>(p.bs.yb) + (okb ? o : 0), okb);
       pf_bm[sl] = (ok && p.bs.mask != nullptr) ? (uint32_t)p.bs.mask[o >> 3] : 0xffu;
     }
   };
@@ -1232,12 +1248,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     for (; k + 12 < splits; k += 16) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = P[(size_t)(k + 4 * q) * n4 + e];
+        const uint4 u = ld16s<SDX_NT_PART != 0>(P + (size_t)(k + 4 * q) * n4 + e);
+        const float4 v = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
         a[q].x += v.x; a[q].y += v.y; a[q].z += v.z; a[q].w += v.w;
       }
     }
     for (; k < splits; k += 4) {
-      const float4 v = P[(size_t)k * n4 + e];
+      const uint4 u = ld16s<SDX_NT_PART != 0>(P + (size_t)k * n4 + e);
+      const float4 v = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
       a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
     }
   }

@@ -200,8 +200,10 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_kernel(W1Params p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = c0 + wn * WN_COLS + 16 * j + 4 * h4;
-      *reinterpret_cast<float4*>(out + (size_t)m * p.C + n) =
-          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      const f32x4 a = acc[i][j];
+      st16<SDX_NT_PART != 0>(out + (size_t)m * p.C + n,
+                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                        __float_as_uint(a[3])));
     }
   }
 }

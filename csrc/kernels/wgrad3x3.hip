@@ -244,8 +244,10 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
     for (int j = 0; j < 9; ++j) {
       const int n = wn * 144 + 16 * j + 4 * h4;
       const int t = n >> 6;
-      *reinterpret_cast<float4*>(out + (size_t)m * Ncol + t * p.C + c0 + (n & 63)) =
-          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      const f32x4 a = acc[i][j];
+      st16<SDX_NT_PART != 0>(out + (size_t)m * Ncol + t * p.C + c0 + (n & 63),
+                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                        __float_as_uint(a[3])));
     }
   }
 }
