@@ -283,7 +283,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
                                                   int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
                                                   OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb,
                                                   OptT mb, OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub,
-                                                  FuseReq* fr) {
+                                                  FuseReq* fr, int store_masked = 0) {
   check_bf16_nhwc(ya, "ya");
   const int64_t C = wt.size(0);
   TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
@@ -323,6 +323,8 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   const int ns = yb.has_value() ? 3 : 2;
   auto slab = torch::empty({rows, ns, C}, dy.options().dtype(at::kFloat));
   bs.slab = slab.data_ptr<float>();
+  TORCH_CHECK(!store_masked || (mask_bits.has_value() && stride == 1), "store_masked: stride-1 with a ReLU bitmask");
+  bs.store_masked = store_masked;
   auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs, addend_sub, fr);
   return {dx, slab};
 }
@@ -330,9 +332,10 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
 std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W,
                                              int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
                                              OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
-                                             OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0) {
+                                             OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0,
+                                             int store_masked = 0) {
   return conv_dgrad_bnstat_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, ya, ma, yb, mb, mask_bits,
-                                msc, msh, addend_sub, nullptr);
+                                msc, msh, addend_sub, nullptr, store_masked);
 }
 
 }  // namespace
@@ -999,6 +1002,70 @@ void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int6
   conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, true, c10::nullopt, c10::nullopt);
 }
 
+// BN3 fold (bnfold.hip): dW3 (+)= diag(A)·G + diag(D)·W3·S + E ⊗ Σa2 with G = dzᵀ·a2 and
+// S = a2ᵀ·a2 (two 1x1 wgrad GEMMs) — on the side stream after the coefficients are known
+void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const torch::Tensor& w3,
+                     const torch::Tensor& coef, const torch::Tensor& sink, int64_t side) {
+  const int64_t C3 = dz.size(3), K3 = a2.size(3);
+  auto body = [&]() {
+    auto opt = coef.options();
+    auto G = torch::empty({C3, 1, 1, K3}, opt);
+    conv_wgrad(dz, a2, 1, 1, 1, 0, 0, -1, G, false, c10::nullopt, c10::nullopt);
+    auto Sm = torch::empty({K3, 1, 1, K3}, opt);
+    conv_wgrad(a2, a2, 1, 1, 1, 0, 0, -1, Sm, false, c10::nullopt, c10::nullopt);
+    auto cs = at::sum(a2.view({-1, K3}), {0}, false, at::kFloat);
+    check_hip(launch_bnfold_wgrad(coef.data_ptr<float>(), G.data_ptr<float>(), Sm.data_ptr<float>(),
+                                  cs.data_ptr<float>(), w3.data_ptr(), (int)C3, (int)K3, sink.data_ptr<float>(), 1,
+                                  cur_stream()),
+              "bnfold_wgrad");
+    if (side != 0) {
+      side_stash().push_back(G);
+      side_stash().push_back(Sm);
+      side_stash().push_back(cs);
+    }
+  };
+  if (side == 0) {
+    body();
+    return;
+  }
+  hipStream_t main = cur_stream();
+  hipStream_t ss = reinterpret_cast<hipStream_t>(side);
+  hipEvent_t ev = next_event();
+  check_hip(hipEventRecord(ev, main), "hipEventRecord");
+  check_hip(hipStreamWaitEvent(ss, ev, 0), "hipStreamWaitEvent");
+  auto hs = c10::hip::getStreamFromExternal(ss, dz.device().index());
+  for (const auto* t : {&dz, &a2, &w3, &coef}) side_stash().push_back(*t);
+  c10::hip::HIPStreamGuard guard(hs);
+  body();
+}
+
+// BN3 fold, main-stream part: Wd = diag(A)·W3 (dgrad layout), then T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3
+// (bf16), the D·y3 + E part of dy3 pushed through conv3's data gradient (added by its epilogue)
+std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor& coef, const torch::Tensor& w3,
+                                                            const torch::Tensor& wt3, const torch::Tensor& a2) {
+  const int64_t C3 = w3.size(0), K3 = w3.size(3);
+  TORCH_CHECK(w3.size(1) == 1 && w3.size(2) == 1 && wt3.size(0) == K3 && wt3.size(3) == C3 && a2.size(3) == K3 &&
+                  coef.numel() == 3 * C3,
+              "bn3 fold: conv3 must be 1x1 [C][1][1][K] with a2 of K channels");
+  auto wd = torch::empty_like(wt3);
+  auto mx = torch::empty({K3, 1, 1, K3}, w3.options());
+  auto b = torch::empty({K3}, coef.options());
+  check_hip(launch_bnfold_prep(coef.data_ptr<float>(), w3.data_ptr(), wt3.data_ptr(), (int)C3, (int)K3, wd.data_ptr(),
+                               mx.data_ptr(), b.data_ptr<float>(), cur_stream()),
+            "bnfold_prep");
+  const int64_t rows = a2.numel() / K3;
+  TORCH_CHECK(rows < (1LL << 31), "bn3 fold: too many rows");
+  ConvGeom g{};
+  g.N = (int)rows; g.H = g.W = 1; g.C = (int)K3; g.K = (int)K3;
+  g.R = g.S = 1; g.P = g.Q = 1; g.stride = 1; g.pad = 0;
+  auto T = torch::empty_like(a2);
+  const GemmEpi epi{b.data_ptr<float>(), 0, 0};
+  check_hip(launch_conv_fwd(g, a2.data_ptr(), mx.data_ptr(), T.data_ptr(), nullptr, auto_cfg(rows, K3, K3, true),
+                            cur_stream(), nullptr, nullptr, &epi),
+            "bnfold T gemm");
+  return {wd, T};
+}
+
 // bn: [gamma, beta, running_mean, running_var] per BN, in the order bn1, bn2, (bn3), (shortcut bn)
 // returns [out, y1, a1, y2, a2|-, y3|-, ys|-, omask (uint8 ReLU bits of out; training only),
 //          then sc, sh, mu, iv per BN]
@@ -1073,7 +1140,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
                                      std::vector<torch::Tensor> bnst, std::vector<torch::Tensor> wt,
                                      std::vector<torch::Tensor> dw, std::vector<torch::Tensor> bng, int64_t stride,
                                      bool bottleneck, bool proj, int64_t side, int64_t comm, OptT in_slab,
-                                     std::vector<torch::Tensor> prev) {
+                                     std::vector<torch::Tensor> prev, std::vector<torch::Tensor> fold_w) {
   const int nconv = bottleneck ? 3 : 2;
   const int nbn = nconv + (proj ? 1 : 0);
   TORCH_CHECK((int)wt.size() == nbn && (int)dw.size() == nbn && (int)bng.size() == 3 * nbn &&
@@ -1090,6 +1157,11 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   torch::Tensor dylast, dys, dz;
   const bool have_slab = in_slab.has_value() && in_slab->defined() && in_slab->numel() > 0;
   if (have_slab) TORCH_CHECK(in_slab->size(1) == (proj ? 3 : 2), "block_bwd: in_slab set count");
+  // BN3 fold (bnfold.hip): fold_w = [conv3 forward weights] was passed because this block
+  // published the fold marker (prev[5]) to the next block, whose final dgrad then stored
+  // dout already masked (dz = dout·[out > 0]) together with in_slab
+  const bool fold = bottleneck && !proj && have_slab && fold_w.size() == 1 && fold_w[0].defined();
+  torch::Tensor coef3;
   if (proj) {
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), G(nconv, 0),
@@ -1107,17 +1179,23 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
                  : bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), c10::nullopt, c10::nullopt, c10::nullopt,
                                c10::nullopt, cnt_last, G(lastbn, 0), S(lastbn, 3), c10::nullopt, c10::nullopt,
                                G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt);
-    // identity shortcut: its gradient dz = dout·[out > 0] is never materialised when the ReLU
-    // bitmask is available — the last dgrad epilogue adds dout under the mask
-    const bool bitmask = out.scalar_type() == at::kByte;
-    auto r = bn_bwd_apply(dout, out, ylast, c[0], c10::nullopt, c10::nullopt, !bitmask, c10::nullopt, c10::nullopt);
-    dylast = r[0];
-    dz = bitmask ? torch::Tensor() : r[2];
+    if (fold) {
+      coef3 = c[0];
+      dz = dout;
+    } else {
+      // identity shortcut: its gradient dz = dout·[out > 0] is never materialised when the ReLU
+      // bitmask is available — the last dgrad epilogue adds dout under the mask
+      const bool bitmask = out.scalar_type() == at::kByte;
+      auto r = bn_bwd_apply(dout, out, ylast, c[0], c10::nullopt, c10::nullopt, !bitmask, c10::nullopt,
+                            c10::nullopt);
+      dylast = r[0];
+      dz = bitmask ? torch::Tensor() : r[2];
+    }
   }
   // dgrad whose output da is the gradient of the block-internal BN i's ReLU output; the BN's
   // Σda·m, Σda·m·(y−μ) come from the dgrad epilogue (SDX_DGRAD_BNSTAT=0: separate pass)
   auto dgrad_bn = [&](const torch::Tensor& dyo, const torch::Tensor& w, const torch::Tensor& y, int64_t st,
-                      int64_t pad, int i, double cnt) -> std::pair<torch::Tensor, torch::Tensor> {
+                      int64_t pad, int i, double cnt, OptT add = c10::nullopt) -> std::pair<torch::Tensor, torch::Tensor> {
     if (dgrad_bnstat_enabled() && st == 1 && stat_fuse_enabled(2)) {
       // the dgrad's last block reduces the statistics and (one rank) evaluates the coefficients
       const bool sync = comm != 0 && small_comm_world(comm) > 1;
@@ -1128,7 +1206,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
         fr.ca = coef_args(y, y.size(3), 1, cnt, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt, c10::nullopt,
                           G(i, 1), G(i, 2), c10::nullopt, c10::nullopt, o);
       }
-      auto r = conv_dgrad_bnstat_impl(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt,
+      auto r = conv_dgrad_bnstat_impl(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, add,
                                       c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0),
                                       S(i, 1), 0, &fr);
       if (!sync) return {r[0], o.coef_a};
@@ -1139,21 +1217,29 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
       return {r[0], c[0]};
     }
     if (dgrad_bnstat_enabled()) {
-      auto r = conv_dgrad_bnstat(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt,
+      auto r = conv_dgrad_bnstat(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, add,
                                  c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0), S(i, 1));
       auto c = bn_bwd_coef_slab(comm, r[1], cnt, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt,
                                 c10::nullopt, G(i, 1), G(i, 2), c10::nullopt, c10::nullopt);
       return {r[0], c[0]};
     }
-    auto da = conv_dgrad(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, c10::nullopt, c10::nullopt);
+    auto da = conv_dgrad(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, add, c10::nullopt);
     auto c = bn_bwd_sync(comm, da, c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, S(i, 0), S(i, 1), cnt,
                          G(i, 0), S(i, 3), c10::nullopt, c10::nullopt, G(i, 1), G(i, 2), c10::nullopt, c10::nullopt);
     return {da, c[0]};
   };
   torch::Tensor dy1;
   if (bottleneck) {
-    side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
-    auto r2 = dgrad_bn(dylast, wt[2], y2, 1, 0, 1, cnt_last);
+    std::pair<torch::Tensor, torch::Tensor> r2;
+    if (fold) {
+      // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
+      auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2);
+      side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side);
+      r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
+    } else {
+      side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
+      r2 = dgrad_bn(dylast, wt[2], y2, 1, 0, 1, cnt_last);
+    }
     auto dy2 = bn_bwd_apply(r2.first, c10::nullopt, y2, r2.second, c10::nullopt, c10::nullopt, false, S(1, 0),
                             S(1, 1))[0];
     side_wgrad(dy2, a1, 3, 3, stride, 1, dw[1], side);
@@ -1170,14 +1256,16 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   }
   const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
   // the final dgrad (the one that stores dx) optionally emits the previous block's output-BN sums
-  const bool want_prev = dgrad_bnstat_enabled() && prev.size() == 5 && prev[4].defined() && prev[4].numel() > 0;
+  const bool want_prev = dgrad_bnstat_enabled() && prev.size() >= 5 && prev[4].defined() && prev[4].numel() > 0;
+  // the previous block folds its BN3 backward: store its dz = dx·[out_prev > 0], not dx
+  const bool prev_fold = want_prev && prev.size() >= 6 && prev[5].defined() && prev[5].numel() > 0;
   torch::Tensor prev_slab;
   auto last_dgrad = [&](OptT o, OptT add, OptT amask, int64_t asub = 0) -> torch::Tensor {
     if (!want_prev) return conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, asub);
     const bool two = prev[2].defined() && prev[2].numel() > 0;
     auto r = conv_dgrad_bnstat(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, prev[0], prev[1],
                                two ? OptT(prev[2]) : OptT(), two ? OptT(prev[3]) : OptT(), prev[4], c10::nullopt,
-                               c10::nullopt, asub);
+                               c10::nullopt, asub, prev_fold ? 1 : 0);
     prev_slab = r[1];
     return r[0];
   };
@@ -1258,7 +1346,7 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("ya"), pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(),
         pybind11::arg("mb") = pybind11::none(), pybind11::arg("mask_bits") = pybind11::none(),
         pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none(),
-        pybind11::arg("addend_sub") = 0);
+        pybind11::arg("addend_sub") = 0, pybind11::arg("store_masked") = 0);
   m.def("bn_bwd_coef_slab", &bn_bwd_coef_slab, "BN-backward coefficients (+dγ/dβ into sinks) from a dgrad stat slab",
         pybind11::arg("comm"), pybind11::arg("slab"), pybind11::arg("count"), pybind11::arg("g_a"),
         pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),
@@ -1273,7 +1361,8 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("dout"), pybind11::arg("saved"), pybind11::arg("bnst"), pybind11::arg("wt"),
         pybind11::arg("dw"), pybind11::arg("bng"), pybind11::arg("stride"), pybind11::arg("bottleneck"),
         pybind11::arg("proj"), pybind11::arg("side"), pybind11::arg("comm") = 0,
-        pybind11::arg("in_slab") = pybind11::none(), pybind11::arg("prev") = std::vector<torch::Tensor>());
+        pybind11::arg("in_slab") = pybind11::none(), pybind11::arg("prev") = std::vector<torch::Tensor>(),
+        pybind11::arg("fold_w") = std::vector<torch::Tensor>());
   m.def("bn_bwd_apply", &bn_bwd_apply, pybind11::arg("dout"), pybind11::arg("outv"), pybind11::arg("ya"),
         pybind11::arg("ca"), pybind11::arg("yb") = pybind11::none(), pybind11::arg("cb") = pybind11::none(),
         pybind11::arg("want_dz") = false, pybind11::arg("msc") = pybind11::none(),

@@ -29,6 +29,15 @@ hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, 
                              float inv_temp, float w, const float* gscale, float* dA, float* dC, float* ws,
                              hipStream_t s);
 
+// ---- BN3 fold of the identity bottleneck backward (bnfold.hip) -----------------
+// coef: [3][C] (A, D, E); w: conv3 forward weights bf16 [C][K]; wt: its dgrad layout [K][C].
+// prep: wd = dgrad layout of diag(A)·W3 [K][C] bf16, mx = W3ᵀ·diag(D)·W3 [K][K] bf16,
+// bias = Eᵀ·W3 [K] fp32. wgrad: sink (+)= diag(A)·G + diag(D)·W3·S + E ⊗ cs ([C][K] fp32).
+hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
+                              float* bias, hipStream_t s);
+hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, const void* w, int C,
+                               int K, float* sink, int accumulate, hipStream_t s);
+
 // ---- implicit-GEMM convolution (igemm.hip) ------------------------------------
 struct ConvGeom {
   int N, H, W, C;   // input NHWC

@@ -21,6 +21,10 @@ using namespace sdx;
 
 namespace {
 
+#ifndef SDX_EW_UNROLL
+#define SDX_EW_UNROLL 1
+#endif
+
 // slab [rows][NS][C] fp32 -> sums [NS][C] fp64 in one launch. grid (ceil(C/64), gy): block
 // (x, y) sums its contiguous row range for 64 channels (4 thread rows, fp64) into
 // scratch[y][NS][C]; it then takes an agent-scope ticket on counters[x], and the block that
@@ -211,7 +215,24 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
   ApplyOp<RES, RELU> op;
   if ((stride % C8) == 0) {
     op.load(sc, sh, sc2, sh2, (e0 % C8) * 8);
-    for (int e = e0; e < n8; e += stride) {
+    int e = e0;
+    // SDX_EW_UNROLL grid-stride iterations per trip: all their loads are issued before
+    // the first store, so each lane keeps U (x2 with a residual) 16-B loads in flight
+    for (; e + (SDX_EW_UNROLL - 1) * stride < n8; e += SDX_EW_UNROLL * stride) {
+      uint4 yv[SDX_EW_UNROLL], rv[SDX_EW_UNROLL];
+#pragma unroll
+      for (int u = 0; u < SDX_EW_UNROLL; ++u) {
+        yv[u] = ld16s<SDX_NT_EW_LOAD != 0>(Y + e + u * stride);
+        rv[u] = RES != 0 ? ld16s<SDX_NT_EW_LOAD != 0>(R + e + u * stride) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < SDX_EW_UNROLL; ++u) {
+        const uint4 o = op.run(yv[u], rv[u]);
+        st16<SDX_NT_EW != 0>(O + e + u * stride, o);
+        if (mask_out) mask_out[e + u * stride] = relu_bits(o);
+      }
+    }
+    for (; e < n8; e += stride) {
       const uint4 o = op.run(ld16s<SDX_NT_EW_LOAD != 0>(Y + e),
                              RES != 0 ? ld16s<SDX_NT_EW_LOAD != 0>(R + e) : make_uint4(0, 0, 0, 0));
       st16<SDX_NT_EW != 0>(O + e, o);
@@ -414,7 +435,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   };
   if ((stride % C8) == 0) {
     op.load(ca, cb, msc, msh, C, (e0 % C8) * 8);
-    for (int e = e0; e < n8; e += stride)
+    int e = e0;
+    for (; e + (SDX_EW_UNROLL - 1) * stride < n8; e += SDX_EW_UNROLL * stride) {
+      uint4 dv[SDX_EW_UNROLL], ov[SDX_EW_UNROLL], av[SDX_EW_UNROLL], bv[SDX_EW_UNROLL];
+#pragma unroll
+      for (int u = 0; u < SDX_EW_UNROLL; ++u) {
+        const int eu = e + u * stride;
+        dv[u] = ld16s<SDX_NT_EW_LOAD != 0>(D + eu);
+        ov[u] = has_out ? ld16s<SDX_NT_EW_LOAD != 0>(OV + eu) : z;
+        av[u] = ld16s<SDX_NT_EW_LOAD != 0>(YA + eu);
+        bv[u] = TWO ? ld16s<SDX_NT_EW_LOAD != 0>(YB + eu) : z;
+      }
+#pragma unroll
+      for (int u = 0; u < SDX_EW_UNROLL; ++u) one(e + u * stride, dv[u], ov[u], av[u], bv[u]);
+    }
+    for (; e < n8; e += stride)
       one(e, ld16s<SDX_NT_EW_LOAD != 0>(D + e), has_out ? ld16s<SDX_NT_EW_LOAD != 0>(OV + e) : z,
           ld16s<SDX_NT_EW_LOAD != 0>(YA + e), TWO ? ld16s<SDX_NT_EW_LOAD != 0>(YB + e) : z);
   } else {
@@ -426,7 +461,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
 }
 
 int ew_grid(long n8) {
-  long g = (n8 + 255) / 256;
+  // enough lanes for SDX_EW_UNROLL elements each, at most 4096 blocks (2 per-CU residencies)
+  long g = (n8 + 256L * SDX_EW_UNROLL - 1) / (256L * SDX_EW_UNROLL);
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   return (int)g;

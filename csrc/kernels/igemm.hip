@@ -1116,7 +1116,8 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
           }
           v = make_uint4(r[0], r[1], r[2], r[3]);
         }
-        st16<SDX_NT_STORE != 0>(out + o, v);
+        // VAR 2 stores once, after the ReLU-backward mask below
+        if (VAR != 2 || !(MODE == MODE_DGRAD && bst)) st16<SDX_NT_STORE != 0>(out + o, v);
         if (MODE == MODE_DGRAD && bst) {
           // statistics of the stored (bf16-rounded) values, as bn_bwd_reduce would read them
           float d[8], ya[8];
@@ -1129,10 +1130,11 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
 #pragma unroll
             for (int q = 0; q < 8; ++q) d[q] = ya[q] * bmk_s[q] + bmk_t[q] > 0.f ? d[q] : 0.f;
           }
-          // VAR 2: ReLU backward applied to the stored gradient too (head: dh = (dz·W2)·[h > 0]):
-          // the chunk is stored again, masked (bf16 values already, so the repack is exact).
-          // Its own variant: the BN-statistics kernels sit at the 128-VGPR occupancy step
-          if constexpr (VAR == 2) *reinterpret_cast<uint4*>(out + o) = pack8(d);
+          // VAR 2: ReLU backward applied to the stored gradient too (head: dh = (dz·W2)·[h > 0];
+          // BN3 fold: dz = dout·[out > 0] of the previous block): the chunk is stored masked
+          // (bf16 values already, so the repack is exact). Its own variant: the
+          // BN-statistics kernels sit at the 128-VGPR occupancy step
+          if constexpr (VAR == 2) st16<SDX_NT_STORE != 0>(out + o, pack8(d));
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             bsum[0][q] += d[q];
@@ -1327,9 +1329,12 @@ template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   const dim3 g(grid), b(64 * WM * WN);
   if (bs && p.bs.store_masked) {
-    // masked-store statistics variant (projection head): 64x64 LDS-DMA tiles only
-    if constexpr (MODE == MODE_DGRAD && BM == 64 && BN == 64 && DEPTH == 3) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, false>), g, b, 0, s, p);
+    // masked-store statistics variant (projection head, BN3 fold): LDS-DMA tiles only
+    if constexpr (MODE == MODE_DGRAD && DEPTH == 3) {
+      if (p.Kdim <= BK && igemm_one())
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, true>), g, b, 0, s, p);
+      else
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, false>), g, b, 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }

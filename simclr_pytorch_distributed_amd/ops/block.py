@@ -335,11 +335,16 @@ class _NativeBlock(torch.autograd.Function):
             ctx.save_for_backward(*saved, *r[8:])
             ctx.blk, ctx.wc, ctx.info, ctx.params, ctx.comm_h = blk, wc, info, params, comm_h
             ctx.link_in, ctx.link_out = link_in, link_out
+            ctx.fold = False
             if link_out is not None:
                 nconv = 3 if bottle else 2
                 st = r[8:]
                 link_out.prev = [r[5] if bottle else r[3], st[4 * (nconv - 1) + 2],
                                  r[6] if proj else e, st[4 * nconv + 2] if proj else _empty_f(x), r[7]]
+                if _fold_eligible(convs, bottle, proj):
+                    # BN3 fold: the next block's final dgrad stores dz = dout·[out > 0] (marker)
+                    link_out.prev.append(_fold_marker(x))
+                    ctx.fold = True
         return out
 
     @staticmethod
@@ -356,9 +361,10 @@ class _NativeBlock(torch.autograd.Function):
         lin, lout = ctx.link_in, ctx.link_out
         in_slab = lout.slab if lout is not None else None
         prev = lin.prev if (lin is not None and lin.prev is not None) else []
+        fold_w = [wc.fwd(convs[2])] if getattr(ctx, "fold", False) else []
         dx, pslab = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
                                 [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side,
-                                ctx.comm_h, in_slab, prev)
+                                ctx.comm_h, in_slab, prev, fold_w)
         if lout is not None:
             lout.slab = lout.prev = None
         if lin is not None:
@@ -368,6 +374,26 @@ class _NativeBlock(torch.autograd.Function):
 
 
 _EMPTY = {}
+_MARK = {}
+
+# BN3 fold of identity bottlenecks (csrc/kernels/bnfold.hip): dy3 = A·dz + D·y3 + E is never
+# materialised — conv3's dgrad runs on dz with diag(A)·W3 plus the fold term
+# T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3 added in its epilogue, and dW3 is rebuilt from dzᵀ·a2 and a2ᵀ·a2.
+# Applied where conv3's input width K is at most SDX_BN3_FOLD_MAXK (the fold matrices cost C·K²;
+# the elementwise pass it removes costs rows·C): layers 1-2 of the CIFAR ResNet-50.
+BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "0") != "0"
+BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "128"))
+
+
+def _fold_eligible(convs, bottle, proj) -> bool:
+    return BN3_FOLD and bottle and not proj and convs[2].kernel_size == (1, 1) and convs[2].in_channels <= BN3_FOLD_MAXK
+
+
+def _fold_marker(like):
+    t = _MARK.get(like.device)
+    if t is None:
+        t = _MARK[like.device] = torch.ones(1, dtype=torch.uint8, device=like.device)
+    return t
 
 
 def _empty_f(like):

@@ -102,8 +102,8 @@ def test_whole_network_gradients_within_bf16_envelope(gpu, name):
     assert not bad, f"{len(bad)} of {len(rows)} gradients outside the bf16 envelope: {bad[:6]}"
 
 
-@pytest.mark.parametrize("name", ["resnet50", "resnet18"])
-def test_block_pairs_gradients_match_fp32(gpu, name):
+@pytest.mark.parametrize("name,fold", [("resnet50", False), ("resnet50", True), ("resnet18", False)])
+def test_block_pairs_gradients_match_fp32(gpu, name, fold, monkeypatch):
     """Teacher-forced backward of every pair of consecutive residual blocks through the
     native executor (so the cross-block hand-off of BN-backward sums from the next
     block's final dgrad epilogue, the compact strided-shortcut gradient and the ReLU
@@ -118,6 +118,9 @@ def test_block_pairs_gradients_match_fp32(gpu, name):
     from simclr_pytorch_distributed_amd.models.resnet import Bottleneck
     from simclr_pytorch_distributed_amd.ops import block as fb
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    # fold: identity bottlenecks of layers 1-2 with the BN3 fold (csrc/kernels/bnfold.hip);
+    # pairs (2,3), (4,5), (6,7) have a folding first block
+    monkeypatch.setattr(fb, "BN3_FOLD", fold)
     nat_m, ref_m = _models(gpu, name)
     flat = FlatParams(nat_m)
     runner = ModelRunner(nat_m, "native", master=flat.flat)
@@ -233,3 +236,49 @@ def test_trajectory_tracks_fp32(gpu):
     for w in range(5):
         tol = max(0.025 * mt[w], 2 * abs(mc[w] - mt[w]))
         assert abs(mn[w] - mt[w]) <= tol, (w, mn[w], mt[w], mc[w])
+
+
+def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
+    """BN3 fold (csrc/kernels/bnfold.hip) vs the materialised dy3 path on the same two-block
+    chains (identity bottleneck -> next block) of ResNet-50 layers 1-2: every parameter
+    gradient and the input gradient agree to bf16 rounding noise (masks are fixed by the
+    forward, so only rounding points differ): rel <= 2e-2, cos >= 0.9998."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner
+    from simclr_pytorch_distributed_amd.ops import block as fb
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    nat_m, ref_m = _models(gpu, "resnet50")
+    flat = FlatParams(nat_m)
+    runner = ModelRunner(nat_m, "native", master=flat.flat)
+    wc = runner.weight_cache()
+    nb = list(nat_m.encoder.blocks())
+    g = torch.Generator().manual_seed(5)
+    bad, seen = [], 0
+    for i in (1, 2, 4, 5, 6):       # l1.1, l1.2, l2.1, l2.2, l2.3: identity, K <= 128
+        c_in = nb[i].conv1.in_channels
+        hw = 32 if i < 3 else 16
+        x = torch.randn(16, hw, hw, c_in, generator=g).relu().to(gpu).to(torch.bfloat16)
+        dy = None
+        res = {}
+        for fold in (False, True):
+            monkeypatch.setattr(fb, "BN3_FOLD", fold)
+            flat.zero_grad()
+            wc.refresh()
+            chain = fb.BlockChain()
+            xn = x.clone().requires_grad_(True)
+            out = fb.bottleneck(fb.bottleneck(xn, nb[i], wc, True, None, chain), nb[i + 1], wc, True, None, chain)
+            if dy is None:
+                dy = torch.randn(out.shape, generator=g).to(gpu).to(torch.bfloat16)
+            out.backward(dy)
+            torch.cuda.synchronize()
+            res[fold] = [xn.grad.float().clone()] + [p.grad.float().clone() for j in (i, i + 1)
+                                                     for p in nb[j].parameters()]
+        names = ["dx"] + [f"block {j} {n}" for j in (i, i + 1) for n, _ in nb[j].named_parameters()]
+        for n, a, b in zip(names, res[True], res[False]):
+            a, b = a.double().flatten(), b.double().flatten()
+            rel = float((a - b).norm() / (b.norm() + 1e-30))
+            cos = float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-30))
+            seen += 1
+            if not (rel <= 2e-2 and cos >= 0.9998):
+                bad.append((f"pair {i}: {n}", round(rel, 5), round(cos, 6)))
+    assert seen > 0
+    assert not bad, bad[:10]
