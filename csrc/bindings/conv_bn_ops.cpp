@@ -1013,15 +1013,20 @@ void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const tor
     conv_wgrad(dz, a2, 1, 1, 1, 0, 0, -1, G, false, c10::nullopt, c10::nullopt);
     auto Sm = torch::empty({K3, 1, 1, K3}, opt);
     conv_wgrad(a2, a2, 1, 1, 1, 0, 0, -1, Sm, false, c10::nullopt, c10::nullopt);
-    auto cs = at::sum(a2.view({-1, K3}), {0}, false, at::kFloat);
+    auto part = torch::empty({bnfold_colsum_blocks(), K3}, opt);
+    auto cs = torch::empty({K3}, opt);
+    check_hip(launch_bnfold_colsum(a2.data_ptr(), a2.numel() / K3, (int)K3, part.data_ptr<float>(),
+                                   cs.data_ptr<float>(), cur_stream()),
+              "bnfold_colsum");
     check_hip(launch_bnfold_wgrad(coef.data_ptr<float>(), G.data_ptr<float>(), Sm.data_ptr<float>(),
-                                  cs.data_ptr<float>(), w3.data_ptr(), (int)C3, (int)K3, sink.data_ptr<float>(), 1,
-                                  cur_stream()),
+                                  cs.data_ptr<float>(), 1, w3.data_ptr(), (int)C3, (int)K3, sink.data_ptr<float>(),
+                                  1, cur_stream()),
               "bnfold_wgrad");
     if (side != 0) {
       side_stash().push_back(G);
       side_stash().push_back(Sm);
       side_stash().push_back(cs);
+      side_stash().push_back(part);
     }
   };
   if (side == 0) {

@@ -35,8 +35,11 @@ hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, 
 // bias = Eᵀ·W3 [K] fp32. wgrad: sink (+)= diag(A)·G + diag(D)·W3·S + E ⊗ cs ([C][K] fp32).
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
                               float* bias, hipStream_t s);
-hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, const void* w, int C,
-                               int K, float* sink, int accumulate, hipStream_t s);
+hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, int ncs,
+                               const void* w, int C, int K, float* sink, int accumulate, hipStream_t s);
+// cs[K] = column sums of a [rows][K] bf16 tensor (partial: [bnfold_colsum_blocks()][K] scratch)
+int bnfold_colsum_blocks();
+hipError_t launch_bnfold_colsum(const void* x, long rows, int K, float* partial, float* cs, hipStream_t s);
 
 // ---- implicit-GEMM convolution (igemm.hip) ------------------------------------
 struct ConvGeom {

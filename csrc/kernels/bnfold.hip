@@ -21,49 +21,114 @@ namespace {
 
 // blocks [0, K): row l of Mx (Mx[l][k] = Σ_c W[c][l]·D[c]·W[c][k], symmetric) and b[l];
 // blocks [K, gridDim.x): Wd[k][c] = A[c]·Wt[k][c] (dgrad layout of diag(A)·W3), grid-stride.
-__global__ __launch_bounds__(256) void bnfold_prep_kernel(const float* __restrict__ coef, const uint16_t* __restrict__ w,
+// A row block splits the C-long reductions over P = NT/K lane groups (K <= NT), each
+// summing every P-th channel with 8 independent loads in flight, then adds the groups.
+constexpr int PREP_NT = 1024;
+__global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __restrict__ coef, const uint16_t* __restrict__ w,
                                                           const uint16_t* __restrict__ wt, int C, int K,
                                                           uint16_t* __restrict__ wd, uint16_t* __restrict__ mx,
                                                           float* __restrict__ bias) {
-  extern __shared__ float sm[];   // [C] W[c][l]·D[c], then [256] reduction
+  extern __shared__ float sm[];   // [C] W[c][l]·D[c], then [PREP_NT] partial sums
   const float* A = coef;
   const float* D = coef + C;
   const float* E = coef + 2 * C;
+  const int t = threadIdx.x;
   if ((int)blockIdx.x < K) {
     const int l = blockIdx.x;
+    float* red = sm + C;
     float eb = 0.f;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    for (int c = t; c < C; c += PREP_NT) {
       const float wl = bf2f(w[(size_t)c * K + l]);
       sm[c] = wl * D[c];
       eb = fmaf(E[c], wl, eb);
     }
-    float* red = sm + C;
-    red[threadIdx.x] = eb;
+    red[t] = eb;
     __syncthreads();
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
-      float acc = 0.f;
-      for (int c = 0; c < C; ++c) acc = fmaf(sm[c], bf2f(w[(size_t)c * K + k]), acc);
-      mx[(size_t)l * K + k] = f2bf(acc);
-    }
-    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
-      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    for (int off = PREP_NT / 2; off > 0; off >>= 1) {
+      if (t < off) red[t] += red[t + off];
       __syncthreads();
     }
-    if (threadIdx.x == 0) bias[l] = red[0];
+    if (t == 0) bias[l] = red[0];
+    __syncthreads();
+    const int KW = K >= PREP_NT ? PREP_NT : K;   // k lanes per group
+    const int P = PREP_NT / KW;                  // lane groups splitting the channel sum
+    const int grp = t / KW;
+    for (int k0 = 0; k0 < K; k0 += KW) {
+      const int k = k0 + t % KW;
+      float acc = 0.f;
+#pragma unroll 8
+      for (int c = grp; c < C; c += P) acc = fmaf(sm[c], bf2f(w[(size_t)c * K + k]), acc);
+      red[t] = acc;
+      __syncthreads();
+      if (grp == 0) {
+        float v = acc;
+        for (int q = 1; q < P; ++q) v += red[t + q * KW];
+        mx[(size_t)l * K + k] = f2bf(v);
+      }
+      __syncthreads();
+    }
     return;
   }
   const long n = (long)K * C;
-  const long stride = (long)(gridDim.x - K) * blockDim.x;
-  for (long e = (long)(blockIdx.x - K) * blockDim.x + threadIdx.x; e < n; e += stride) {
+  const long stride = (long)(gridDim.x - K) * PREP_NT;
+  for (long e = (long)(blockIdx.x - K) * PREP_NT + t; e < n; e += stride) {
     const int c = (int)(e % C);
     wd[e] = f2bf(A[c] * bf2f(wt[e]));
   }
 }
 
-// sink[c][k] (+)= A[c]·G[c][k] + D[c]·Σ_l W[c][l]·S[l][k] + E[c]·cs[k]; one block per c
+// per-block column sums of a [rows][K] bf16 tensor: partial[blockIdx][K] (fp32). Lanes keep
+// a fixed 8-channel group (the grid stride is a multiple of K/8).
+__global__ __launch_bounds__(256) void bnfold_colsum_kernel(const uint16_t* __restrict__ x, long n8, int K,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[256][9];
+  const int K8 = K / 8;
+  const long stride = (long)gridDim.x * 256;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n8; e += stride) {
+    float v[8];
+    unpack8(ld16s<true>(reinterpret_cast<const uint4*>(x) + e), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += v[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[threadIdx.x][i] = acc[i];
+  __syncthreads();
+  if ((int)threadIdx.x < K8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int q = threadIdx.x; q < 256; q += K8)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += red[q][i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) partial[(size_t)blockIdx.x * K + threadIdx.x * 8 + i] = s[i];
+  }
+}
+
+// cs[k] = Σ_b partial[b][k]: a block per 64 columns, 16 lane groups over b, then LDS
+__global__ __launch_bounds__(1024) void bnfold_colsum_finish_kernel(const float* __restrict__ partial, int nb, int K,
+                                                                    float* __restrict__ cs) {
+  __shared__ float red[16][64];
+  const int kl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + kl;
+  float s = 0.f;
+  if (k < K) {
+#pragma unroll 4
+    for (int b = grp; b < nb; b += 16) s += partial[(size_t)b * K + k];
+  }
+  red[grp][kl] = s;
+  __syncthreads();
+  if (grp == 0 && k < K) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += red[q][kl];
+    cs[k] = v;
+  }
+}
+
+// sink[c][k] (+)= A[c]·G[c][k] + D[c]·Σ_l W[c][l]·S[l][k] + E[c]·Σ_b cs[b][k]; one block per c
 __global__ __launch_bounds__(256) void bnfold_wgrad_kernel(const float* __restrict__ coef, const float* __restrict__ G,
                                                            const float* __restrict__ S, const float* __restrict__ cs,
-                                                           const uint16_t* __restrict__ w, int C, int K,
+                                                           int ncs, const uint16_t* __restrict__ w, int C, int K,
                                                            float* __restrict__ sink, int accumulate) {
   extern __shared__ float wrow[];   // [K] W[c][:]
   const int c = blockIdx.x;
@@ -71,10 +136,13 @@ __global__ __launch_bounds__(256) void bnfold_wgrad_kernel(const float* __restri
   __syncthreads();
   const float a = coef[c], d = coef[C + c], e = coef[2 * C + c];
   for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    float ws = 0.f;
+    float ws = 0.f, sk = 0.f;
+#pragma unroll 8
     for (int l = 0; l < K; ++l) ws = fmaf(wrow[l], S[(size_t)l * K + k], ws);
+#pragma unroll 8
+    for (int b = 0; b < ncs; ++b) sk += cs[(size_t)b * K + k];
     const size_t o = (size_t)c * K + k;
-    const float v = a * G[o] + d * ws + e * cs[k];
+    const float v = a * G[o] + d * ws + e * sk;
     sink[o] = accumulate ? sink[o] + v : v;
   }
 }
@@ -83,22 +151,36 @@ __global__ __launch_bounds__(256) void bnfold_wgrad_kernel(const float* __restri
 
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
                               float* bias, hipStream_t s) {
-  if (C <= 0 || K <= 0 || C > 8192) return hipErrorInvalidValue;
+  if (C <= 0 || K <= 0 || C > 8192 || (K < PREP_NT ? PREP_NT % K : K % PREP_NT) != 0) return hipErrorInvalidValue;
   const long n = (long)K * C;
-  int gw = (int)((n + 255) / 256);
-  if (gw > 512) gw = 512;
-  const size_t lds = (size_t)(C + 256) * sizeof(float);
-  hipLaunchKernelGGL(bnfold_prep_kernel, dim3(K + gw), dim3(256), lds, s, coef, (const uint16_t*)w,
+  int gw = (int)((n + PREP_NT - 1) / PREP_NT);
+  if (gw > 256) gw = 256;
+  const size_t lds = (size_t)(C + PREP_NT) * sizeof(float);
+  hipLaunchKernelGGL(bnfold_prep_kernel, dim3(K + gw), dim3(PREP_NT), lds, s, coef, (const uint16_t*)w,
                      (const uint16_t*)wt, C, K, (uint16_t*)wd, (uint16_t*)mx, bias);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
 
-hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, const void* w, int C,
-                               int K, float* sink, int accumulate, hipStream_t s) {
-  if (C <= 0 || K <= 0 || K > 8192) return hipErrorInvalidValue;
+// cs: [ncs][K] partial column sums of a2 (launch_bnfold_colsum)
+hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, int ncs,
+                               const void* w, int C, int K, float* sink, int accumulate, hipStream_t s) {
+  if (C <= 0 || K <= 0 || K > 8192 || ncs <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(bnfold_wgrad_kernel, dim3(C), dim3(K < 256 ? ((K + 63) / 64) * 64 : 256),
-                     (size_t)K * sizeof(float), s, coef, G, S, cs, (const uint16_t*)w, C, K, sink, accumulate);
+                     (size_t)K * sizeof(float), s, coef, G, S, cs, ncs, (const uint16_t*)w, C, K, sink, accumulate);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+int bnfold_colsum_blocks() { return 512; }
+
+// cs[K] fp32 = column sums of x [rows][K] bf16; partial: [bnfold_colsum_blocks()][K] scratch
+hipError_t launch_bnfold_colsum(const void* x, long rows, int K, float* partial, float* cs, hipStream_t s) {
+  if (K % 8 != 0 || K > 2048 || 256 % (K / 8) != 0) return hipErrorInvalidValue;
+  const int nb = bnfold_colsum_blocks();
+  hipLaunchKernelGGL(bnfold_colsum_kernel, dim3(nb), dim3(256), 0, s, (const uint16_t*)x, rows * K / 8, K, partial);
+  SDX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bnfold_colsum_finish_kernel, dim3((K + 63) / 64), dim3(1024), 0, s, partial, nb, K, cs);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -381,7 +381,7 @@ _MARK = {}
 # T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3 added in its epilogue, and dW3 is rebuilt from dzᵀ·a2 and a2ᵀ·a2.
 # Applied where conv3's input width K is at most SDX_BN3_FOLD_MAXK (the fold matrices cost C·K²;
 # the elementwise pass it removes costs rows·C): layers 1-2 of the CIFAR ResNet-50.
-BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "0") != "0"
+BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "1") != "0"
 BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "128"))
 
 
