@@ -1165,8 +1165,11 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   // BN3 fold (bnfold.hip): fold_w = [conv3 forward weights] was passed because this block
   // published the fold marker (prev[5]) to the next block, whose final dgrad then stored
   // dout already masked (dz = dout·[out > 0]) together with in_slab
-  const bool fold = bottleneck && !proj && have_slab && fold_w.size() == 1 && fold_w[0].defined();
-  torch::Tensor coef3;
+  // projection blocks fold both BNs (fold_w = [conv3, shortcut] forward weights; stride-1
+  // shortcut only: its input is then x itself)
+  const bool fold = bottleneck && have_slab && fold_w.size() == (proj ? 2u : 1u) && fold_w[0].defined() &&
+                    (!proj || (stride == 1 && fold_w[1].defined()));
+  torch::Tensor coef3, coefs;
   if (proj) {
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), G(nconv, 0),
@@ -1174,9 +1177,15 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
                  : bn_bwd_sync(comm, dout, out, ylast, S(lastbn, 2), ys, S(nconv, 2), c10::nullopt, c10::nullopt,
                                cnt_last, G(lastbn, 0), S(lastbn, 3), G(nconv, 0), S(nconv, 3), G(lastbn, 1),
                                G(lastbn, 2), G(nconv, 1), G(nconv, 2));
-    auto r = bn_bwd_apply(dout, out, ylast, c[0], ys, c[1], false, c10::nullopt, c10::nullopt);
-    dylast = r[0];
-    dys = r[1];
+    if (fold) {
+      coef3 = c[0];
+      coefs = c[1];
+      dz = dout;
+    } else {
+      auto r = bn_bwd_apply(dout, out, ylast, c[0], ys, c[1], false, c10::nullopt, c10::nullopt);
+      dylast = r[0];
+      dys = r[1];
+    }
   } else {
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), c10::nullopt,
@@ -1275,7 +1284,13 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     return r[0];
   };
   torch::Tensor dx;
-  if (proj) {
+  if (proj && fold) {
+    // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
+    auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x);
+    side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side);
+    dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
+    dx = last_dgrad(dx, dx, c10::nullopt);
+  } else if (proj) {
     side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);
     if (stride > 1 && sub_addend_enabled()) {
       // the strided 1x1 shortcut's data gradient lives on the stride-s subgrid only: compute

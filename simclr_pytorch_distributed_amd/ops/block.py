@@ -361,7 +361,7 @@ class _NativeBlock(torch.autograd.Function):
         lin, lout = ctx.link_in, ctx.link_out
         in_slab = lout.slab if lout is not None else None
         prev = lin.prev if (lin is not None and lin.prev is not None) else []
-        fold_w = [wc.fwd(convs[2])] if getattr(ctx, "fold", False) else []
+        fold_w = [wc.fwd(cv) for cv in convs[2:]] if getattr(ctx, "fold", False) else []
         dx, pslab = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
                                 [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side,
                                 ctx.comm_h, in_slab, prev, fold_w)
@@ -386,7 +386,14 @@ BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "128"))
 
 
 def _fold_eligible(convs, bottle, proj) -> bool:
-    return BN3_FOLD and bottle and not proj and convs[2].kernel_size == (1, 1) and convs[2].in_channels <= BN3_FOLD_MAXK
+    """Identity bottlenecks, and projection bottlenecks whose 1x1 shortcut has stride 1 (then
+    the shortcut BN is folded the same way, over the block input)."""
+    if not (BN3_FOLD and bottle and convs[2].kernel_size == (1, 1) and convs[2].in_channels <= BN3_FOLD_MAXK):
+        return False
+    if not proj:
+        return True
+    sc = convs[3]
+    return sc.kernel_size == (1, 1) and sc.stride == (1, 1) and sc.in_channels <= BN3_FOLD_MAXK
 
 
 def _fold_marker(like):

@@ -240,7 +240,7 @@ def test_trajectory_tracks_fp32(gpu):
 
 def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
     """BN3 fold (csrc/kernels/bnfold.hip) vs the materialised dy3 path on the same two-block
-    chains (identity bottleneck -> next block) of ResNet-50 layers 1-2: every parameter
+    chains (folding bottleneck -> next block) of ResNet-50 layers 1-2: every parameter
     gradient and the input gradient agree to bf16 rounding noise (masks are fixed by the
     forward, so only rounding points differ): rel <= 2e-2, cos >= 0.9998."""
     from simclr_pytorch_distributed_amd.models.executor import ModelRunner
@@ -253,7 +253,8 @@ def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
     nb = list(nat_m.encoder.blocks())
     g = torch.Generator().manual_seed(5)
     bad, seen = [], 0
-    for i in (1, 2, 4, 5, 6):       # l1.1, l1.2, l2.1, l2.2, l2.3: identity, K <= 128
+    # l1.0 (projection, stride-1 shortcut: both BNs folded); l1.1, l1.2, l2.1-l2.3 (identity)
+    for i in (0, 1, 2, 4, 5, 6):
         c_in = nb[i].conv1.in_channels
         hw = 32 if i < 3 else 16
         x = torch.randn(16, hw, hw, c_in, generator=g).relu().to(gpu).to(torch.bfloat16)
