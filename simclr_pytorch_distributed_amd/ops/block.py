@@ -341,7 +341,7 @@ class _NativeBlock(torch.autograd.Function):
                 st = r[8:]
                 link_out.prev = [r[5] if bottle else r[3], st[4 * (nconv - 1) + 2],
                                  r[6] if proj else e, st[4 * nconv + 2] if proj else _empty_f(x), r[7]]
-                if _fold_eligible(convs, bottle, proj):
+                if _fold_eligible(convs, bottle, proj, r[0].shape[0] * r[0].shape[1] * r[0].shape[2]):
                     # BN3 fold: the next block's final dgrad stores dz = dout·[out > 0] (marker)
                     link_out.prev.append(_fold_marker(x))
                     ctx.fold = True
@@ -382,18 +382,28 @@ _MARK = {}
 # Applied where conv3's input width K is at most SDX_BN3_FOLD_MAXK (the fold matrices cost C·K²;
 # the elementwise pass it removes costs rows·C): layers 1-2 of the CIFAR ResNet-50.
 BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "1") != "0"
-BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "128"))
+BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "512"))
+# the fold's fixed cost grows as K² (its C x K x K matrices, the K x K Gram), the pass it
+# removes as rows: fold when rows >= MIN_ROWS_PER_K2 · K². CIFAR 512 views: layers 1-2
+# (128, 8 rows per K²) fold, layer 3 (0.5) does not; 224x224 1024 views: layers 1-3
+BN3_FOLD_ROWS_PER_K2 = float(os.environ.get("SDX_BN3_FOLD_ROWS_PER_K2", "2"))
 
 
-def _fold_eligible(convs, bottle, proj) -> bool:
+def _fold_eligible(convs, bottle, proj, rows) -> bool:
     """Identity bottlenecks, and projection bottlenecks whose 1x1 shortcut has stride 1 (then
     the shortcut BN is folded the same way, over the block input)."""
-    if not (BN3_FOLD and bottle and convs[2].kernel_size == (1, 1) and convs[2].in_channels <= BN3_FOLD_MAXK):
+    if not (BN3_FOLD and bottle):
+        return False
+    k = convs[2].in_channels
+    if not (convs[2].kernel_size == (1, 1) and k <= BN3_FOLD_MAXK
+            and rows >= BN3_FOLD_ROWS_PER_K2 * k * k):
         return False
     if not proj:
         return True
     sc = convs[3]
-    return sc.kernel_size == (1, 1) and sc.stride == (1, 1) and sc.in_channels <= BN3_FOLD_MAXK
+    ks = sc.in_channels
+    return (sc.kernel_size == (1, 1) and sc.stride == (1, 1) and ks <= BN3_FOLD_MAXK
+            and rows >= BN3_FOLD_ROWS_PER_K2 * ks * ks)
 
 
 def _fold_marker(like):

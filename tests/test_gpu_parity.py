@@ -121,6 +121,8 @@ def test_block_pairs_gradients_match_fp32(gpu, name, fold, monkeypatch):
     # fold: identity bottlenecks of layers 1-2 with the BN3 fold (csrc/kernels/bnfold.hip);
     # pairs (2,3), (4,5), (6,7) have a folding first block
     monkeypatch.setattr(fb, "BN3_FOLD", fold)
+    monkeypatch.setattr(fb, "BN3_FOLD_ROWS_PER_K2", 0.0)   # fold at this small batch too
+    monkeypatch.setattr(fb, "BN3_FOLD_MAXK", 128)
     nat_m, ref_m = _models(gpu, name)
     flat = FlatParams(nat_m)
     runner = ModelRunner(nat_m, "native", master=flat.flat)
@@ -246,6 +248,7 @@ def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
     from simclr_pytorch_distributed_amd.models.executor import ModelRunner
     from simclr_pytorch_distributed_amd.ops import block as fb
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    monkeypatch.setattr(fb, "BN3_FOLD_ROWS_PER_K2", 0.0)   # fold at this small batch too
     nat_m, ref_m = _models(gpu, "resnet50")
     flat = FlatParams(nat_m)
     runner = ModelRunner(nat_m, "native", master=flat.flat)
@@ -253,10 +256,11 @@ def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
     nb = list(nat_m.encoder.blocks())
     g = torch.Generator().manual_seed(5)
     bad, seen = [], 0
-    # l1.0 (projection, stride-1 shortcut: both BNs folded); l1.1, l1.2, l2.1-l2.3 (identity)
-    for i in (0, 1, 2, 4, 5, 6):
+    # l1.0 (projection, stride-1 shortcut: both BNs folded); l1.1, l1.2, l2.1-l2.3, l3.1
+    # (identity; K = 64, 128, 256)
+    for i in (0, 1, 2, 4, 5, 6, 8):
         c_in = nb[i].conv1.in_channels
-        hw = 32 if i < 3 else 16
+        hw = 32 if i < 3 else (16 if i < 7 else 8)
         x = torch.randn(16, hw, hw, c_in, generator=g).relu().to(gpu).to(torch.bfloat16)
         dy = None
         res = {}
