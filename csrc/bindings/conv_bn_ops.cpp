@@ -1165,10 +1165,11 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   // BN3 fold (bnfold.hip): fold_w = [conv3 forward weights] was passed because this block
   // published the fold marker (prev[5]) to the next block, whose final dgrad then stored
   // dout already masked (dz = dout·[out > 0]) together with in_slab
-  // projection blocks fold both BNs (fold_w = [conv3, shortcut] forward weights; stride-1
-  // shortcut only: its input is then x itself)
-  const bool fold = bottleneck && have_slab && fold_w.size() == (proj ? 2u : 1u) && fold_w[0].defined() &&
-                    (!proj || (stride == 1 && fold_w[1].defined()));
+  // projection blocks: fold_w = [conv3, shortcut] folds both BNs (stride-1 shortcut only: its
+  // input is then x itself); fold_w = [conv3] folds BN3 and materialises only the shortcut's dys
+  const bool fold = bottleneck && have_slab && !fold_w.empty() && fold_w.size() <= (proj ? 2u : 1u) &&
+                    fold_w[0].defined() && (fold_w.size() == 1 || (stride == 1 && fold_w[1].defined()));
+  const bool fold_sc = fold && proj && fold_w.size() == 2;
   torch::Tensor coef3, coefs;
   if (proj) {
     auto c = have_slab
@@ -1179,8 +1180,12 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
                                G(lastbn, 2), G(nconv, 1), G(nconv, 2));
     if (fold) {
       coef3 = c[0];
-      coefs = c[1];
       dz = dout;
+      if (fold_sc)
+        coefs = c[1];
+      else   // dout is already masked: dys = A'·dz + D'·ys + E' without a ReLU mask
+        dys = bn_bwd_apply(dz, c10::nullopt, ys, c[1], c10::nullopt, c10::nullopt, false, c10::nullopt,
+                           c10::nullopt)[0];
     } else {
       auto r = bn_bwd_apply(dout, out, ylast, c[0], ys, c[1], false, c10::nullopt, c10::nullopt);
       dylast = r[0];
@@ -1284,7 +1289,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     return r[0];
   };
   torch::Tensor dx;
-  if (proj && fold) {
+  if (fold_sc) {
     // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
     auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x);
     side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side);

@@ -335,16 +335,17 @@ class _NativeBlock(torch.autograd.Function):
             ctx.save_for_backward(*saved, *r[8:])
             ctx.blk, ctx.wc, ctx.info, ctx.params, ctx.comm_h = blk, wc, info, params, comm_h
             ctx.link_in, ctx.link_out = link_in, link_out
-            ctx.fold = False
+            ctx.fold = 0   # conv weights folded in backward: 0, 1 (conv3) or 2 (conv3 + shortcut)
             if link_out is not None:
                 nconv = 3 if bottle else 2
                 st = r[8:]
                 link_out.prev = [r[5] if bottle else r[3], st[4 * (nconv - 1) + 2],
                                  r[6] if proj else e, st[4 * nconv + 2] if proj else _empty_f(x), r[7]]
-                if _fold_eligible(convs, bottle, proj, r[0].shape[0] * r[0].shape[1] * r[0].shape[2]):
+                rows = r[0].shape[0] * r[0].shape[1] * r[0].shape[2]
+                if _fold_eligible(convs, bottle, proj, rows):
                     # BN3 fold: the next block's final dgrad stores dz = dout·[out > 0] (marker)
                     link_out.prev.append(_fold_marker(x))
-                    ctx.fold = True
+                    ctx.fold = 2 if (proj and _fold_shortcut(convs, rows)) else 1
         return out
 
     @staticmethod
@@ -361,7 +362,8 @@ class _NativeBlock(torch.autograd.Function):
         lin, lout = ctx.link_in, ctx.link_out
         in_slab = lout.slab if lout is not None else None
         prev = lin.prev if (lin is not None and lin.prev is not None) else []
-        fold_w = [wc.fwd(cv) for cv in convs[2:]] if getattr(ctx, "fold", False) else []
+        nfold = getattr(ctx, "fold", 0)
+        fold_w = [wc.fwd(cv) for cv in convs[2:2 + nfold]]
         dx, pslab = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
                                 [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side,
                                 ctx.comm_h, in_slab, prev, fold_w)
@@ -390,16 +392,19 @@ BN3_FOLD_ROWS_PER_K2 = float(os.environ.get("SDX_BN3_FOLD_ROWS_PER_K2", "2"))
 
 
 def _fold_eligible(convs, bottle, proj, rows) -> bool:
-    """Identity bottlenecks, and projection bottlenecks whose 1x1 shortcut has stride 1 (then
-    the shortcut BN is folded the same way, over the block input)."""
+    """BN3 of a bottleneck (identity or projection); see _fold_shortcut for the shortcut BN."""
     if not (BN3_FOLD and bottle):
         return False
     k = convs[2].in_channels
     if not (convs[2].kernel_size == (1, 1) and k <= BN3_FOLD_MAXK
             and rows >= BN3_FOLD_ROWS_PER_K2 * k * k):
         return False
-    if not proj:
-        return True
+    return True
+
+
+def _fold_shortcut(convs, rows) -> bool:
+    """A projection bottleneck's 1x1 shortcut BN folds the same way over the block input when
+    the shortcut has stride 1 (else its dys is materialised from the already-masked dz)."""
     sc = convs[3]
     ks = sc.in_channels
     return (sc.kernel_size == (1, 1) and sc.stride == (1, 1) and ks <= BN3_FOLD_MAXK

@@ -256,11 +256,11 @@ def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
     nb = list(nat_m.encoder.blocks())
     g = torch.Generator().manual_seed(5)
     bad, seen = [], 0
-    # l1.0 (projection, stride-1 shortcut: both BNs folded); l1.1, l1.2, l2.1-l2.3, l3.1
-    # (identity; K = 64, 128, 256)
-    for i in (0, 1, 2, 4, 5, 6, 8):
+    # l1.0 (projection, stride-1 shortcut: both BNs folded); l2.0 (strided projection: BN3
+    # folded, dys from the masked dz); l1.1, l1.2, l2.1-l2.3, l3.1 (identity; K = 64, 128, 256)
+    for i in (0, 1, 2, 3, 4, 5, 6, 8):
         c_in = nb[i].conv1.in_channels
-        hw = 32 if i < 3 else (16 if i < 7 else 8)
+        hw = 32 if i < 4 else (16 if i < 7 else 8)   # block inputs (l2.0 reads 32x32)
         x = torch.randn(16, hw, hw, c_in, generator=g).relu().to(gpu).to(torch.bfloat16)
         dy = None
         res = {}
