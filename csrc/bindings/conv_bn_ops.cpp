@@ -1004,20 +1004,52 @@ void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int6
 
 // BN3 fold (bnfold.hip): dW3 (+)= diag(A)·G + diag(D)·W3·S + E ⊗ Σa2 with G = dzᵀ·a2 and
 // S = a2ᵀ·a2 (two 1x1 wgrad GEMMs) — on the side stream after the coefficients are known
+// S = a2ᵀ·a2 [K][1][1][K] and cs = Σ_rows a2 [K] (fp32) on the current stream
+std::vector<torch::Tensor> fold_gram_now(const torch::Tensor& a2) {
+  const int64_t K3 = a2.size(3);
+  auto opt = a2.options().dtype(at::kFloat);
+  auto Sm = torch::empty({K3, 1, 1, K3}, opt);
+  conv_wgrad(a2, a2, 1, 1, 1, 0, 0, -1, Sm, false, c10::nullopt, c10::nullopt);
+  auto part = torch::empty({bnfold_colsum_blocks(), K3}, opt);
+  auto cs = torch::empty({K3}, opt);
+  check_hip(launch_bnfold_colsum(a2.data_ptr(), a2.numel() / K3, (int)K3, part.data_ptr<float>(), cs.data_ptr<float>(),
+                                 cur_stream()),
+            "bnfold_colsum");
+  return {Sm, cs, part};
+}
+
+// the Gram of a folded conv's input, issued at forward time on the (then idle) side stream;
+// backward consumes it on the same stream (FIFO), so no further synchronisation is needed
+std::vector<torch::Tensor> fold_gram(torch::Tensor a2, int64_t side) {
+  check_bf16_nhwc(a2, "a2");
+  if (side == 0) return fold_gram_now(a2);
+  hipEvent_t ev = next_event();
+  check_hip(hipEventRecord(ev, cur_stream()), "hipEventRecord");
+  hipStream_t ss = reinterpret_cast<hipStream_t>(side);
+  check_hip(hipStreamWaitEvent(ss, ev, 0), "hipStreamWaitEvent");
+  side_stash().push_back(a2);
+  c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(ss, a2.device().index()));
+  return fold_gram_now(a2);
+}
+
 void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const torch::Tensor& w3,
-                     const torch::Tensor& coef, const torch::Tensor& sink, int64_t side) {
+                     const torch::Tensor& coef, const torch::Tensor& sink, int64_t side,
+                     const torch::Tensor* gram = nullptr) {
   const int64_t C3 = dz.size(3), K3 = a2.size(3);
   auto body = [&]() {
     auto opt = coef.options();
     auto G = torch::empty({C3, 1, 1, K3}, opt);
     conv_wgrad(dz, a2, 1, 1, 1, 0, 0, -1, G, false, c10::nullopt, c10::nullopt);
-    auto Sm = torch::empty({K3, 1, 1, K3}, opt);
-    conv_wgrad(a2, a2, 1, 1, 1, 0, 0, -1, Sm, false, c10::nullopt, c10::nullopt);
-    auto part = torch::empty({bnfold_colsum_blocks(), K3}, opt);
-    auto cs = torch::empty({K3}, opt);
-    check_hip(launch_bnfold_colsum(a2.data_ptr(), a2.numel() / K3, (int)K3, part.data_ptr<float>(),
-                                   cs.data_ptr<float>(), cur_stream()),
-              "bnfold_colsum");
+    torch::Tensor Sm, cs, part;
+    if (gram != nullptr) {
+      Sm = gram[0];
+      cs = gram[1];
+    } else {
+      auto g3 = fold_gram_now(a2);
+      Sm = g3[0];
+      cs = g3[1];
+      part = g3[2];
+    }
     check_hip(launch_bnfold_wgrad(coef.data_ptr<float>(), G.data_ptr<float>(), Sm.data_ptr<float>(),
                                   cs.data_ptr<float>(), 1, w3.data_ptr(), (int)C3, (int)K3, sink.data_ptr<float>(),
                                   1, cur_stream()),
@@ -1026,7 +1058,7 @@ void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const tor
       side_stash().push_back(G);
       side_stash().push_back(Sm);
       side_stash().push_back(cs);
-      side_stash().push_back(part);
+      if (part.defined()) side_stash().push_back(part);
     }
   };
   if (side == 0) {
@@ -1167,9 +1199,15 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   // dout already masked (dz = dout·[out > 0]) together with in_slab
   // projection blocks: fold_w = [conv3, shortcut] folds both BNs (stride-1 shortcut only: its
   // input is then x itself); fold_w = [conv3] folds BN3 and materialises only the shortcut's dys
-  const bool fold = bottleneck && have_slab && !fold_w.empty() && fold_w.size() <= (proj ? 2u : 1u) &&
-                    fold_w[0].defined() && (fold_w.size() == 1 || (stride == 1 && fold_w[1].defined()));
-  const bool fold_sc = fold && proj && fold_w.size() == 2;
+  // fold_w may be followed by the forward-time Grams of the folded convs' inputs (fold_gram):
+  // [W3, (Ws)] or [W3, (Ws), S3, cs3, (Ss, css)]
+  const size_t nfw = fold_w.size() == 3 || fold_w.size() == 6 ? fold_w.size() / 3 : fold_w.size();
+  const bool grams = nfw != fold_w.size();
+  const bool fold = bottleneck && have_slab && nfw >= 1 && nfw <= (proj ? 2u : 1u) && fold_w[0].defined() &&
+                    (nfw == 1 || (stride == 1 && fold_w[1].defined()));
+  const bool fold_sc = fold && proj && nfw == 2;
+  const torch::Tensor* gram3 = grams ? &fold_w[nfw] : nullptr;
+  const torch::Tensor* grams_sc = grams && nfw == 2 ? &fold_w[nfw + 2] : nullptr;
   torch::Tensor coef3, coefs;
   if (proj) {
     auto c = have_slab
@@ -1253,7 +1291,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     if (fold) {
       // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
       auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2);
-      side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side);
+      side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3);
       r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
     } else {
       side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
@@ -1292,7 +1330,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   if (fold_sc) {
     // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
     auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x);
-    side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side);
+    side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side, grams_sc);
     dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
     dx = last_dgrad(dx, dx, c10::nullopt);
   } else if (proj) {
@@ -1382,6 +1420,9 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bn"), pybind11::arg("stride"),
         pybind11::arg("bottleneck"), pybind11::arg("proj"), pybind11::arg("training"), pybind11::arg("eps"),
         pybind11::arg("momentum"), pybind11::arg("comm") = 0);
+  m.def("fold_gram", &fold_gram,
+        "BN3 fold: [a2ᵀ·a2, Σ_rows a2, scratch] of a folded conv's input, issued on the side stream",
+        pybind11::arg("a2"), pybind11::arg("side"));
   m.def("block_bwd", &block_bwd, "native residual-block backward (dgrad chain + side-stream wgrads)",
         pybind11::arg("dout"), pybind11::arg("saved"), pybind11::arg("bnst"), pybind11::arg("wt"),
         pybind11::arg("dw"), pybind11::arg("bng"), pybind11::arg("stride"), pybind11::arg("bottleneck"),

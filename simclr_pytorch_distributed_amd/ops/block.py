@@ -346,6 +346,11 @@ class _NativeBlock(torch.autograd.Function):
                     # BN3 fold: the next block's final dgrad stores dz = dout·[out > 0] (marker)
                     link_out.prev.append(_fold_marker(x))
                     ctx.fold = 2 if (proj and _fold_shortcut(convs, rows)) else 1
+                    if FOLD_GRAM_FWD:
+                        # the folded convs' input Grams on the side stream, idle in forward
+                        from . import streams
+                        side = streams.side(x.device).cuda_stream if streams.ENABLED else 0
+                        ctx.grams = m.fold_gram(r[4], side)[:2] + (m.fold_gram(x, side)[:2] if ctx.fold == 2 else [])
         return out
 
     @staticmethod
@@ -363,7 +368,7 @@ class _NativeBlock(torch.autograd.Function):
         in_slab = lout.slab if lout is not None else None
         prev = lin.prev if (lin is not None and lin.prev is not None) else []
         nfold = getattr(ctx, "fold", 0)
-        fold_w = [wc.fwd(cv) for cv in convs[2:2 + nfold]]
+        fold_w = [wc.fwd(cv) for cv in convs[2:2 + nfold]] + (getattr(ctx, "grams", None) or [])
         dx, pslab = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
                                 [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side,
                                 ctx.comm_h, in_slab, prev, fold_w)
@@ -389,6 +394,9 @@ BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "512"))
 # removes as rows: fold when rows >= MIN_ROWS_PER_K2 · K². CIFAR 512 views: layers 1-2
 # (128, 8 rows per K²) fold, layer 3 (0.5) does not; 224x224 1024 views: layers 1-3
 BN3_FOLD_ROWS_PER_K2 = float(os.environ.get("SDX_BN3_FOLD_ROWS_PER_K2", "2"))
+# the fold's Gram a2ᵀ·a2 and column sums computed at forward time on the side stream
+# (opt-in: measured neutral to slower, 12.47/12.48 vs 12.50/12.59 ms; profiles/bn3_fold_r2.txt)
+FOLD_GRAM_FWD = os.environ.get("SDX_FOLD_GRAM_FWD", "0") != "0"
 
 
 def _fold_eligible(convs, bottle, proj, rows) -> bool:
