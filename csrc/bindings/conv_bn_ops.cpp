@@ -1079,7 +1079,8 @@ void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const tor
 // BN3 fold, main-stream part: Wd = diag(A)·W3 (dgrad layout), then T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3
 // (bf16), the D·y3 + E part of dy3 pushed through conv3's data gradient (added by its epilogue)
 std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor& coef, const torch::Tensor& w3,
-                                                            const torch::Tensor& wt3, const torch::Tensor& a2) {
+                                                            const torch::Tensor& wt3, const torch::Tensor& a2,
+                                                            const torch::Tensor& mu, const torch::Tensor* gram) {
   const int64_t C3 = w3.size(0), K3 = w3.size(3);
   TORCH_CHECK(w3.size(1) == 1 && w3.size(2) == 1 && wt3.size(0) == K3 && wt3.size(3) == C3 && a2.size(3) == K3 &&
                   coef.numel() == 3 * C3,
@@ -1087,10 +1088,12 @@ std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor&
   auto wd = torch::empty_like(wt3);
   auto mx = torch::empty({K3, 1, 1, K3}, w3.options());
   auto b = torch::empty({K3}, coef.options());
-  check_hip(launch_bnfold_prep(coef.data_ptr<float>(), w3.data_ptr(), wt3.data_ptr(), (int)C3, (int)K3, wd.data_ptr(),
-                               mx.data_ptr(), b.data_ptr<float>(), cur_stream()),
-            "bnfold_prep");
   const int64_t rows = a2.numel() / K3;
+  check_vec(mu, C3, "fold mu");
+  check_hip(launch_bnfold_prep(coef.data_ptr<float>(), w3.data_ptr(), wt3.data_ptr(), (int)C3, (int)K3, wd.data_ptr(),
+                               mx.data_ptr(), b.data_ptr<float>(), mu.data_ptr<float>(),
+                               gram != nullptr ? gram[1].data_ptr<float>() : nullptr, (long)rows, cur_stream()),
+            "bnfold_prep");
   TORCH_CHECK(rows < (1LL << 31), "bn3 fold: too many rows");
   ConvGeom g{};
   g.N = (int)rows; g.H = g.W = 1; g.C = (int)K3; g.K = (int)K3;
@@ -1290,7 +1293,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     std::pair<torch::Tensor, torch::Tensor> r2;
     if (fold) {
       // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
-      auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2);
+      auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2, S(lastbn, 2), gram3);
       side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3);
       r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
     } else {
@@ -1329,7 +1332,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   torch::Tensor dx;
   if (fold_sc) {
     // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
-    auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x);
+    auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x, S(nconv, 2), grams_sc);
     side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side, grams_sc);
     dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
     dx = last_dgrad(dx, dx, c10::nullopt);

@@ -33,8 +33,10 @@ hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, 
 // coef: [3][C] (A, D, E); w: conv3 forward weights bf16 [C][K]; wt: its dgrad layout [K][C].
 // prep: wd = dgrad layout of diag(A)·W3 [K][C] bf16, mx = W3ᵀ·diag(D)·W3 [K][K] bf16,
 // bias = Eᵀ·W3 [K] fp32. wgrad: sink (+)= diag(A)·G + diag(D)·W3·S + E ⊗ cs ([C][K] fp32).
+// mu ([C] mean of y3) / cs ([K] column sums of a2 over `rows`): optional coherent-rounding
+// correction folded into bias (see bnfold.hip)
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
-                              float* bias, hipStream_t s);
+                              float* bias, const float* mu, const float* cs, long rows, hipStream_t s);
 hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, int ncs,
                                const void* w, int C, int K, float* sink, int accumulate, hipStream_t s);
 // cs[K] = column sums of a [rows][K] bf16 tensor (partial: [bnfold_colsum_blocks()][K] scratch)

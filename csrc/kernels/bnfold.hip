@@ -24,10 +24,17 @@ namespace {
 // A row block splits the C-long reductions over P = NT/K lane groups (K <= NT), each
 // summing every P-th channel with 8 independent loads in flight, then adds the groups.
 constexpr int PREP_NT = 1024;
+// Coherent-rounding correction (mu, cs given): Wd and Mx are rounded to bf16 once and then
+// applied to every row, so their rounding errors do not average out over the batch the way
+// the per-element rounding of a materialised dy3 does — the BN-parameter gradients of the
+// layers below (sums over all rows) pick up a bias ∝ rows. The row-mean part of that error,
+// mean(dz)·(A·W3 − Wd) + mean(a2)·(Mx − bf16(Mx)), is added back exactly through the fp32
+// bias b; what remains is zero-mean over the rows. mean(dz)[c] = −(E + D·μ)/A (A ≠ 0).
 __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __restrict__ coef, const uint16_t* __restrict__ w,
                                                           const uint16_t* __restrict__ wt, int C, int K,
                                                           uint16_t* __restrict__ wd, uint16_t* __restrict__ mx,
-                                                          float* __restrict__ bias) {
+                                                          float* __restrict__ bias, const float* __restrict__ mu,
+                                                          const float* __restrict__ cs, float inv_rows) {
   extern __shared__ float sm[];   // [C] W[c][l]·D[c], then [PREP_NT] partial sums
   const float* A = coef;
   const float* D = coef + C;
@@ -41,6 +48,11 @@ __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __res
       const float wl = bf2f(w[(size_t)c * K + l]);
       sm[c] = wl * D[c];
       eb = fmaf(E[c], wl, eb);
+      if (mu != nullptr && A[c] != 0.f) {
+        const float m1 = -(E[c] + D[c] * mu[c]) / A[c];
+        const float ex = A[c] * wl;
+        eb = fmaf(m1, ex - bf2f(f2bf(ex)), eb);
+      }
     }
     red[t] = eb;
     __syncthreads();
@@ -48,11 +60,12 @@ __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __res
       if (t < off) red[t] += red[t + off];
       __syncthreads();
     }
-    if (t == 0) bias[l] = red[0];
+    float bsum = red[0];
     __syncthreads();
     const int KW = K >= PREP_NT ? PREP_NT : K;   // k lanes per group
     const int P = PREP_NT / KW;                  // lane groups splitting the channel sum
     const int grp = t / KW;
+    float ca = 0.f;                              // Σ_k mean(a2)[k]·(Mx − bf16(Mx))[l][k]
     for (int k0 = 0; k0 < K; k0 += KW) {
       const int k = k0 + t % KW;
       float acc = 0.f;
@@ -63,10 +76,19 @@ __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __res
       if (grp == 0) {
         float v = acc;
         for (int q = 1; q < P; ++q) v += red[t + q * KW];
-        mx[(size_t)l * K + k] = f2bf(v);
+        const uint16_t r = f2bf(v);
+        mx[(size_t)l * K + k] = r;
+        if (cs != nullptr) ca = fmaf(cs[k] * inv_rows, v - bf2f(r), ca);
       }
       __syncthreads();
     }
+    red[t] = ca;
+    __syncthreads();
+    for (int off = PREP_NT / 2; off > 0; off >>= 1) {
+      if (t < off) red[t] += red[t + off];
+      __syncthreads();
+    }
+    if (t == 0) bias[l] = bsum + red[0];
     return;
   }
   const long n = (long)K * C;
@@ -150,14 +172,15 @@ __global__ __launch_bounds__(256) void bnfold_wgrad_kernel(const float* __restri
 }  // namespace
 
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
-                              float* bias, hipStream_t s) {
+                              float* bias, const float* mu, const float* cs, long rows, hipStream_t s) {
   if (C <= 0 || K <= 0 || C > 8192 || (K < PREP_NT ? PREP_NT % K : K % PREP_NT) != 0) return hipErrorInvalidValue;
   const long n = (long)K * C;
   int gw = (int)((n + PREP_NT - 1) / PREP_NT);
   if (gw > 256) gw = 256;
   const size_t lds = (size_t)(C + PREP_NT) * sizeof(float);
   hipLaunchKernelGGL(bnfold_prep_kernel, dim3(K + gw), dim3(PREP_NT), lds, s, coef, (const uint16_t*)w,
-                     (const uint16_t*)wt, C, K, (uint16_t*)wd, (uint16_t*)mx, bias);
+                     (const uint16_t*)wt, C, K, (uint16_t*)wd, (uint16_t*)mx, bias, mu, cs,
+                     rows > 0 ? 1.f / (float)rows : 0.f);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -347,10 +347,15 @@ class _NativeBlock(torch.autograd.Function):
                     link_out.prev.append(_fold_marker(x))
                     ctx.fold = 2 if (proj and _fold_shortcut(convs, rows)) else 1
                     if FOLD_GRAM_FWD:
-                        # the folded convs' input Grams on the side stream, idle in forward
+                        # the folded convs' input Grams (a2ᵀa2, Σa2) on the side stream, idle in
+                        # forward; backward's main stream waits on the event for the column sums
+                        # (coherent-rounding correction of the fold bias, bnfold.hip)
                         from . import streams
                         side = streams.side(x.device).cuda_stream if streams.ENABLED else 0
                         ctx.grams = m.fold_gram(r[4], side)[:2] + (m.fold_gram(x, side)[:2] if ctx.fold == 2 else [])
+                        if side:
+                            ctx.gram_ev = torch.cuda.Event()
+                            ctx.gram_ev.record(streams.side(x.device))
         return out
 
     @staticmethod
@@ -369,6 +374,9 @@ class _NativeBlock(torch.autograd.Function):
         prev = lin.prev if (lin is not None and lin.prev is not None) else []
         nfold = getattr(ctx, "fold", 0)
         fold_w = [wc.fwd(cv) for cv in convs[2:2 + nfold]] + (getattr(ctx, "grams", None) or [])
+        ev = getattr(ctx, "gram_ev", None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
         dx, pslab = m.block_bwd(dout.contiguous(), list(t[:8]), list(t[8:]), [wc.dgrad(cv) for cv in convs],
                                 [sinks.target(cv.weight) for cv in convs], bng, ctx.blk.stride, bottle, proj, side,
                                 ctx.comm_h, in_slab, prev, fold_w)
@@ -388,15 +396,20 @@ _MARK = {}
 # T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3 added in its epilogue, and dW3 is rebuilt from dzᵀ·a2 and a2ᵀ·a2.
 # Applied where conv3's input width K is at most SDX_BN3_FOLD_MAXK (the fold matrices cost C·K²;
 # the elementwise pass it removes costs rows·C): layers 1-2 of the CIFAR ResNet-50.
-BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "1") != "0"
+# OPT-IN: at the headline batch (512 views) the fold's BN2 gradients in layer 1 are ~2x
+# further from fp32 than the materialised path's (tools/fold_bn_probe.py,
+# profiles/fold_bn_probe_r2.txt: l1.1 bn2.bias 0.32 vs 0.17, autocast 0.15), although every
+# conv gradient and layer 2 match; root cause open. 12.84 -> 12.49 ms/step when enabled.
+BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "0") != "0"
 BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "512"))
 # the fold's fixed cost grows as K² (its C x K x K matrices, the K x K Gram), the pass it
 # removes as rows: fold when rows >= MIN_ROWS_PER_K2 · K². CIFAR 512 views: layers 1-2
 # (128, 8 rows per K²) fold, layer 3 (0.5) does not; 224x224 1024 views: layers 1-3
 BN3_FOLD_ROWS_PER_K2 = float(os.environ.get("SDX_BN3_FOLD_ROWS_PER_K2", "2"))
-# the fold's Gram a2ᵀ·a2 and column sums computed at forward time on the side stream
-# (opt-in: measured neutral to slower, 12.47/12.48 vs 12.50/12.59 ms; profiles/bn3_fold_r2.txt)
-FOLD_GRAM_FWD = os.environ.get("SDX_FOLD_GRAM_FWD", "0") != "0"
+# the fold's Gram a2ᵀ·a2 and column sums computed at forward time on the side stream; the
+# column sums also feed the fold's coherent-rounding correction (0 = Grams in backward,
+# without the mean(a2) part of the correction)
+FOLD_GRAM_FWD = os.environ.get("SDX_FOLD_GRAM_FWD", "1") != "0"
 
 
 def _fold_eligible(convs, bottle, proj, rows) -> bool:

@@ -287,3 +287,36 @@ def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
                 bad.append((f"pair {i}: {n}", round(rel, 5), round(cos, 6)))
     assert seen > 0
     assert not bad, bad[:10]
+
+
+@pytest.mark.xfail(strict=False, reason="open: the opt-in BN3 fold's layer-1 BN2 gradients drift from the "
+                   "materialised path at 512 views (profiles/fold_bn_probe_r2.txt)")
+def test_bn3_fold_full_batch_gradients(gpu, monkeypatch):
+    """The BN3 fold at the headline batch (512 views of 32x32, where its Grams and column
+    sums run over 524288 rows in layer 1): whole-network parameter gradients, fold vs the
+    materialised dy3 path, same weights / input / forward (masks identical) — every one of
+    the 161 parameters within bf16 rounding noise (rel <= 3e-2, cos >= 0.9995)."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
+    from simclr_pytorch_distributed_amd.ops import block as fb
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    nat_m, _ = _models(gpu, "resnet50")
+    flat = FlatParams(nat_m)
+    runner = ModelRunner(nat_m, "native", master=flat.flat)
+    x = to_nhwc_input(_images(gpu, 512, seed=4))
+    G = torch.randn(512, 128, generator=torch.Generator().manual_seed(6)).to(gpu)
+    grads = {}
+    for fold in (False, True):
+        monkeypatch.setattr(fb, "BN3_FOLD", fold)
+        flat.zero_grad()
+        (runner.forward(x) * G).sum().backward()
+        torch.cuda.synchronize()
+        grads[fold] = [p.grad.double().flatten().clone() for p in nat_m.parameters()]
+    bad, worst = [], (0.0, "")
+    for (n, _), a, b in zip(nat_m.named_parameters(), grads[True], grads[False]):
+        rel = float((a - b).norm() / (b.norm() + 1e-30))
+        cos = float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-30))
+        worst = max(worst, (rel, f"{n}: rel {rel:.4g} cos {cos:.6f}"))
+        if not (rel <= 3e-2 and cos >= 0.9995):
+            bad.append((n, round(rel, 5), round(cos, 6)))
+    print(f"fold vs unfolded at 512 views, worst: {worst[1]}")
+    assert not bad, bad[:10]
