@@ -191,6 +191,12 @@ std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t st
 }
 
 // bs (optional): fused BN-backward statistics; its slab must hold conv_dgrad_slab_rows rows
+// set around the BN3 fold's conv3 dgrad (block_bwd): its T addend is added before rounding
+int& fold_add_pre() {
+  thread_local int on = 0;
+  return on;
+}
+
 torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                               int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
                               c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0,
@@ -246,8 +252,11 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     StatFuse sf{};
     torch::Tensor lvl2;
     if (fr != nullptr) sf = make_fuse(*fr, dy, M, g.C, (int)cfg, bs->yb != nullptr ? 3 : 2, lvl2);
+    // BN3 fold: the addend joins the accumulators before rounding (kernels built with SDX_ADD_PRE)
+    static const GemmEpi pre{nullptr, 0, 0, 1};
+    const GemmEpi* epi = (fold_add_pre() && add != nullptr && addend_sub == 0 && amask == nullptr) ? &pre : nullptr;
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0, nullptr,
+                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0, epi,
                                       fr != nullptr ? &sf : nullptr),
               "conv_dgrad");
     return dx;
@@ -1295,7 +1304,9 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
       // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
       auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2, S(lastbn, 2), gram3);
       side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3);
+      fold_add_pre() = 1;
       r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
+      fold_add_pre() = 0;
     } else {
       side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
       r2 = dgrad_bn(dylast, wt[2], y2, 1, 0, 1, cnt_last);
@@ -1334,7 +1345,9 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
     auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x, S(nconv, 2), grams_sc);
     side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side, grams_sc);
+    fold_add_pre() = 1;
     dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
+    fold_add_pre() = 0;
     dx = last_dgrad(dx, dx, c10::nullopt);
   } else if (proj) {
     side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);

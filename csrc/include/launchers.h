@@ -73,6 +73,9 @@ struct GemmEpi {
   const float* bias;
   int relu;
   int out_f32;
+  // DGRAD (stride 1): add the bf16 addend to the fp32 accumulators before the single bf16
+  // rounding instead of after it (builds with SDX_ADD_PRE=1; BN3 fold experiment)
+  int add_pre;
 };
 int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);

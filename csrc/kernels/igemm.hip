@@ -46,6 +46,12 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
+#ifndef SDX_ADD_PRE
+// DGRAD addend added to the fp32 accumulators before rounding when the launch asks for it
+// (GemmEpi::add_pre, BN3 fold): without it the fold's small mean-removal addend is swamped
+// by the bf16 rounding of the main term (profiles/bn3_fold_r2.txt)
+#define SDX_ADD_PRE 1
+#endif
 #ifndef SDX_NT_LOAD
 // non-temporal loads of the dgrad epilogue's read-once operands (addend, BN inputs): step
 // 13.15 -> 13.05 ms on the same box (profiles/nt_store_r2.txt); 0 = cached loads
@@ -89,6 +95,7 @@ struct IgemmParams {
   // rows stored straight from the accumulators (no bf16 rounding, no BN statistics)
   const float* bias;
   int relu, out_f32;
+  int add_pre;   // GemmEpi::add_pre
   // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
   int worder;
   // FWD statistics / DGRAD BN-backward statistics reduced in-kernel (sf.cnt != nullptr)
@@ -978,6 +985,28 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     return;
   }
 
+#if SDX_ADD_PRE
+  if (MODE == MODE_DGRAD && p.add_pre && p.addend != nullptr) {
+    // the addend joins the fp32 accumulators, so the sum is rounded to bf16 once (a small
+    // addend added after rounding is swamped: profiles/bn3_fold_r2.txt). Stride-1 rows.
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = m0 + wm * WTM + 16 * i + c;
+      if (row >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WTN + 16 * j + 4 * h;
+        if (col < p.Ncol) {
+          const uint2 a = *reinterpret_cast<const uint2*>(p.addend + (size_t)row * p.Ncol + col);
+          acc[i][j][0] += __uint_as_float(a.x << 16);
+          acc[i][j][1] += __uint_as_float(a.x & 0xffff0000u);
+          acc[i][j][2] += __uint_as_float(a.y << 16);
+          acc[i][j][3] += __uint_as_float(a.y & 0xffff0000u);
+        }
+      }
+    }
+  }
+#endif
   // bf16 rounding (stats describe the stored tensor); pack 4 consecutive columns
   uint2 ov[TM][TN];
 #pragma unroll
@@ -995,7 +1024,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   constexpr int ITER = BM * CPR / NT;
   constexpr int PF = ITER < 4 ? ITER : 4;
   static_assert(NT % CPR == 0 && CPR <= 64 && (BM * CPR) % NT == 0, "fixed column chunk per thread");
-  const bool has_add = MODE == MODE_DGRAD && p.addend != nullptr;
+  const bool has_add = MODE == MODE_DGRAD && p.addend != nullptr && !(SDX_ADD_PRE && p.add_pre);
   constexpr bool bst = MODE == MODE_DGRAD && VAR != 0;
   const int my_ch = tid % CPR, my_col = n0 + my_ch * 8;
   int eo[ITER];   // output element offset of each chunk (-1: outside the tensor)
@@ -1470,6 +1499,7 @@ void set_epi(IgemmParams& p, const GemmEpi* epi) {
   p.bias = epi->bias;
   p.relu = epi->relu;
   p.out_f32 = epi->out_f32;
+  p.add_pre = epi->add_pre;
 }
 }  // namespace
 

@@ -396,11 +396,11 @@ _MARK = {}
 # T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3 added in its epilogue, and dW3 is rebuilt from dzᵀ·a2 and a2ᵀ·a2.
 # Applied where conv3's input width K is at most SDX_BN3_FOLD_MAXK (the fold matrices cost C·K²;
 # the elementwise pass it removes costs rows·C): layers 1-2 of the CIFAR ResNet-50.
-# OPT-IN: at the headline batch (512 views) the fold's BN2 gradients in layer 1 are ~2x
-# further from fp32 than the materialised path's (tools/fold_bn_probe.py,
-# profiles/fold_bn_probe_r2.txt: l1.1 bn2.bias 0.32 vs 0.17, autocast 0.15), although every
-# conv gradient and layer 2 match; root cause open. 12.84 -> 12.49 ms/step when enabled.
-BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "0") != "0"
+# The fold's addend T enters conv3's dgrad accumulators before the bf16 rounding
+# (GemmEpi::add_pre): added after it, T was swamped and the layer-1 BN2 gradients drifted
+# at 512 views (l1.1 bn2.bias 0.32 vs 0.17 rel to fp32); with it they are at 0.166 vs 0.170
+# materialised (tools/fold_bn_probe.py, profiles/bn3_fold_r2.txt).
+BN3_FOLD = os.environ.get("SDX_BN3_FOLD", "1") != "0"
 BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "512"))
 # the fold's fixed cost grows as K² (its C x K x K matrices, the K x K Gram), the pass it
 # removes as rows: fold when rows >= MIN_ROWS_PER_K2 · K². CIFAR 512 views: layers 1-2
