@@ -407,9 +407,10 @@ BN3_FOLD_MAXK = int(os.environ.get("SDX_BN3_FOLD_MAXK", "512"))
 # (128, 8 rows per K²) fold, layer 3 (0.5) does not; 224x224 1024 views: layers 1-3
 BN3_FOLD_ROWS_PER_K2 = float(os.environ.get("SDX_BN3_FOLD_ROWS_PER_K2", "2"))
 # the fold's Gram a2ᵀ·a2 and column sums computed at forward time on the side stream; the
-# column sums also feed the fold's coherent-rounding correction (0 = Grams in backward,
-# without the mean(a2) part of the correction)
-FOLD_GRAM_FWD = os.environ.get("SDX_FOLD_GRAM_FWD", "1") != "0"
+# column sums also feed the mean(a2) part of the fold bias's rounding correction. Opt-in:
+# with the accumulator pre-add the correction is not needed (full-batch worst 0.033 rel either
+# way) and Grams in backward are faster (12.53 vs 12.60 ms, profiles/bn3_fold_r2.txt)
+FOLD_GRAM_FWD = os.environ.get("SDX_FOLD_GRAM_FWD", "0") != "0"
 
 
 def _fold_eligible(convs, bottle, proj, rows) -> bool:
