@@ -38,7 +38,33 @@ sys.path.insert(0, ROOT)
 METRIC = "images/sec (whole node) SimCLR ResNet-50 BS=256; CIFAR-10 linear-probe top-1"
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start one rank per GPU through
+    torch.distributed.run as a CHILD process (never an exec: nothing here has touched the
+    GPU, and the parent stays alive to relay), pass rank 0's JSON line through, and return
+    the child's exit status. Reference launch recipe: run_supcon.sh:4-11."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ, SDX_BENCH_CHILD="1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    n_req = pre.parse_known_args()[0].gpus
+    if n_req > 1 and "WORLD_SIZE" not in os.environ and not os.environ.get("SDX_BENCH_CHILD"):
+        raise SystemExit(_self_launch(n_req))
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)

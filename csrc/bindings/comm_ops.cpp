@@ -13,6 +13,14 @@
 //   kind EMU   — W virtual ranks holding identical data in ONE process (tests): the sum is
 //                x·W, so every SyncBN code path of the executor runs on a single GPU and
 //                must reproduce the single-process result.
+//   kind XEMU  — EMU semantics, but the executor's BN statistics take the FUSED xGMI path
+//                (bn.hip col_reduce + exchange): W virtual ranks are W z-slices of each
+//                launch exchanging through W arenas in device memory (xgmi_emu_create).
+//
+// Fused SyncBN exchange (kinds XGMI / XEMU): small_comm_fused() hands the executor the
+// arena arguments of one exchange; the column reduction of the BN statistics then stores,
+// exchanges and sums them and runs the finalize / coefficient epilogue in the same launch
+// (one launch per BN instead of reduce + collective + finalize).
 //
 // Failure handling. The RCCL communicator is created NON-blocking
 // (config.blocking = 0): initialisation is polled against a deadline and aborted on
@@ -60,13 +68,16 @@ namespace sdx_bind {
 torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x);
 int64_t xgmi_world(int64_t id);
 int64_t xgmi_error_ext(int64_t id);
+int64_t xgmi_error_nothrow(int64_t id);
+int64_t xgmi_emu_create_ext(int64_t world, int64_t cap, double timeout_s);
+XgmiCol xgmi_col_args(int64_t id);
 
 namespace {
 
 using Clock = std::chrono::steady_clock;
 constexpr int kCommFailureExit = 3;   // utils/faults.py COLLECTIVE_FAILURE_EXIT_CODE
 
-enum Kind { KIND_RCCL = 1, KIND_XGMI = 2, KIND_EMU = 3 };
+enum Kind { KIND_RCCL = 1, KIND_XGMI = 2, KIND_EMU = 3, KIND_XEMU = 4 };
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
@@ -123,42 +134,57 @@ std::shared_ptr<SmallComm> get(int64_t h) {
 std::atomic<bool> g_stop{false};
 std::thread* g_thread = nullptr;   // leaked on purpose (joined by the atexit hook)
 
+void sweep() {
+  Registry& R = reg();
+  std::lock_guard<std::mutex> lk(R.mu);
+  for (auto& c : R.comms) {
+    if (!c || c->world <= 1) continue;
+    if (c->kind == KIND_XGMI || c->kind == KIND_XEMU) {
+      const int64_t e = xgmi_error_nothrow(c->xgmi_id);
+      if (e != 0) {
+        char buf[200];
+        std::snprintf(buf, sizeof(buf), "flag of peer rank %d missed the %.0f s deadline (arena %lld)", (int)e - 1,
+                      c->timeout_s, (long long)c->xgmi_id);
+        fail_exit(*c, buf);
+      }
+    }
+    if (c->kind == KIND_RCCL && c->nccl) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+        fail_exit(*c, ncclGetErrorString(ae));
+    }
+    if (!c->armed.load(std::memory_order_acquire)) continue;
+    const hipError_t q = hipEventQuery(c->ev);
+    if (q == hipSuccess) {
+      continue;
+    } else if (q == hipErrorNotReady) {
+      const double waited = 1e-9 * (double)(now_ns() - c->armed_at.load());
+      if (waited > c->timeout_s) {
+        char buf[160];
+        std::snprintf(buf, sizeof(buf), "a collective did not complete within %.1f s (a peer died or stalled)",
+                      c->timeout_s);
+        fail_exit(*c, buf);
+      }
+    } else {
+      fail_exit(*c, hipGetErrorString(q));
+    }
+  }
+}
+
+// the whole sweep holds the registry lock, so small_comm_destroy / abort never tear down
+// a communicator under it
 void watchdog_loop() {
   while (!g_stop.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
     if (g_stop.load()) break;
-    // the whole sweep holds the registry lock, so small_comm_destroy never tears down a
-    // communicator under it
-    Registry& R = reg();
-    std::lock_guard<std::mutex> lk(R.mu);
-    for (auto& c : R.comms) {
-      if (!c || c->world <= 1) continue;
-      if (c->kind == KIND_XGMI && xgmi_error_ext(c->xgmi_id) != 0) {
-        char buf[200];
-        std::snprintf(buf, sizeof(buf), "flag of peer rank %d missed the %.0f s deadline (arena %lld)",
-                      (int)xgmi_error_ext(c->xgmi_id) - 1, c->timeout_s, (long long)c->xgmi_id);
-        fail_exit(*c, buf);
-      }
-      if (c->kind == KIND_RCCL && c->nccl) {
-        ncclResult_t ae = ncclSuccess;
-        if (ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
-          fail_exit(*c, ncclGetErrorString(ae));
-      }
-      if (!c->armed.load(std::memory_order_acquire)) continue;
-      const hipError_t q = hipEventQuery(c->ev);
-      if (q == hipSuccess) {
-        continue;
-      } else if (q == hipErrorNotReady) {
-        const double waited = 1e-9 * (double)(now_ns() - c->armed_at.load());
-        if (waited > c->timeout_s) {
-          char buf[160];
-          std::snprintf(buf, sizeof(buf), "a collective did not complete within %.1f s (a peer died or stalled)",
-                        c->timeout_s);
-          fail_exit(*c, buf);
-        }
-      } else {
-        fail_exit(*c, hipGetErrorString(q));
-      }
+    // (an exception must never leave this detached thread: std::terminate would take
+    // the process down without the diagnostic)
+    try {
+      sweep();
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "native communicator watchdog: sweep error ignored: %s\n", e.what());
+    } catch (...) {
+      std::fprintf(stderr, "native communicator watchdog: sweep error ignored\n");
     }
   }
 }
@@ -207,6 +233,23 @@ int64_t add(std::shared_ptr<SmallComm> c) {
   return (int64_t)R.comms.size();
 }
 
+// SDX_SYNCBN_FUSED=0: the xGMI kinds fall back to reduce -> one-shot all-reduce -> finalize
+bool fused_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("SDX_SYNCBN_FUSED");
+    return e != nullptr && atoi(e) == 0;
+  }();
+  return off;
+}
+
+// abort + clear the RCCL communicator under the registry lock: the watchdog sweep reads
+// c.nccl under that lock, so it never queries a communicator mid-abort
+void abort_locked(SmallComm& c) {
+  std::lock_guard<std::mutex> lk(reg().mu);
+  if (c.nccl) (void)ncclCommAbort(c.nccl);
+  c.nccl = nullptr;
+}
+
 // poll a non-blocking communicator until its pending operation settles (deadline)
 void settle(SmallComm& c, ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return;
@@ -217,13 +260,11 @@ void settle(SmallComm& c, ncclResult_t r, const char* what) {
     check_nccl(ncclCommGetAsyncError(c.nccl, &ae), "ncclCommGetAsyncError");
     if (ae == ncclSuccess) return;
     if (ae != ncclInProgress) {
-      (void)ncclCommAbort(c.nccl);
-      c.nccl = nullptr;
+      abort_locked(c);
       TORCH_CHECK(false, what, " failed: ", ncclGetErrorString(ae));
     }
     if (std::chrono::duration<double>(Clock::now() - t0).count() > c.timeout_s) {
-      (void)ncclCommAbort(c.nccl);
-      c.nccl = nullptr;
+      abort_locked(c);
       TORCH_CHECK(false, what, " timed out after ", c.timeout_s, " s (a peer rank did not join or stalled)");
     }
     std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -272,6 +313,17 @@ int64_t xgmi_small_comm(int64_t xgmi_id, int64_t rank, double timeout_s) {
   c->rank = (int)rank;
   c->timeout_s = timeout_s;
   check_hip(hipGetDevice(&c->device), "hipGetDevice");
+  return add(std::move(c));
+}
+
+int64_t xgmi_emu_small_comm(int64_t world, double timeout_s) {
+  TORCH_CHECK(world >= 1 && world <= kXgmiMaxPeers, "1 <= world <= 8");
+  auto c = std::make_shared<SmallComm>();
+  c->kind = KIND_XEMU;
+  c->world = (int)world;
+  c->timeout_s = timeout_s;
+  check_hip(hipGetDevice(&c->device), "hipGetDevice");
+  c->xgmi_id = xgmi_emu_create_ext(world, 12288, timeout_s);
   return add(std::move(c));
 }
 
@@ -347,7 +399,7 @@ SmallComm& gather_comm(int64_t h, const torch::Tensor& x, const char* what) {
   SmallComm& c = *get(h);
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.device().index() == c.device, what,
               ": contiguous tensor on the communicator's device");
-  TORCH_CHECK(c.kind == KIND_RCCL || c.kind == KIND_EMU, what, ": RCCL or emulated communicator only");
+  TORCH_CHECK(c.kind != KIND_XGMI, what, ": RCCL or emulated communicator only");
   if (c.kind == KIND_RCCL) TORCH_CHECK(c.nccl, what, ": RCCL communicator was aborted");
   return c;
 }
@@ -443,6 +495,22 @@ torch::Tensor rownorm_gather_bwd(int64_t h, torch::Tensor gC, torch::Tensor y, t
 
 int small_comm_world(int64_t h) { return h == 0 ? 1 : get(h)->world; }
 
+// fused SyncBN exchange (XGMI / XEMU kinds of >1 ranks): the arena arguments of ONE exchange
+// (epoch advanced); false for any other communicator (reduce -> small_all_reduce_ -> finalize)
+bool small_comm_fused(int64_t h, XgmiCol* out) {
+  if (h == 0) return false;
+  auto cp = get(h);
+  if (cp->world <= 1 || (cp->kind != KIND_XGMI && cp->kind != KIND_XEMU) || fused_disabled()) return false;
+  *out = xgmi_col_args(cp->xgmi_id);
+  return true;
+}
+
+// after the fused launch was enqueued on the current stream: watchdog event behind it
+void small_comm_fused_issued(int64_t h) {
+  auto cp = get(h);
+  arm(*cp, cur_stream());
+}
+
 // in-place SUM over the communicator's ranks, ordered on the current stream
 void small_all_reduce_(int64_t h, torch::Tensor& x) {
   if (h == 0) return;
@@ -463,7 +531,7 @@ void small_all_reduce_(int64_t h, torch::Tensor& x) {
       default: TORCH_CHECK(false, "small all-reduce: fp64 / fp32 / int32 only");
     }
     settle(c, ncclAllReduce(x.data_ptr(), x.data_ptr(), (size_t)x.numel(), dt, ncclSum, c.nccl, s), "ncclAllReduce");
-  } else if (c.kind == KIND_EMU) {
+  } else if (c.kind == KIND_EMU || c.kind == KIND_XEMU) {
     x.mul_((double)c.world);
   } else {
     TORCH_CHECK(x.scalar_type() == at::kDouble, "xGMI small all-reduce: fp64 only");
@@ -480,6 +548,9 @@ void register_comm(pybind11::module& m) {
         pybind11::arg("id"), pybind11::arg("world"), pybind11::arg("rank"), pybind11::arg("timeout_s") = 600.0);
   m.def("xgmi_small_comm", &xgmi_small_comm, "wrap a one-shot xGMI arena as a small-communicator handle",
         pybind11::arg("xgmi_id"), pybind11::arg("rank"), pybind11::arg("timeout_s") = 600.0);
+  m.def("xgmi_emu_small_comm", &xgmi_emu_small_comm,
+        "W identical virtual ranks whose BN statistics take the fused xGMI exchange (W arenas on this device)",
+        pybind11::arg("world"), pybind11::arg("timeout_s") = 10.0);
   m.def("emu_small_comm", &emu_small_comm, "W identical virtual ranks in one process (tests): sum = x*W",
         pybind11::arg("world"), pybind11::arg("timeout_s") = 600.0);
   m.def("small_comm_destroy", &small_comm_destroy);
@@ -487,7 +558,7 @@ void register_comm(pybind11::module& m) {
   m.def("small_comm_world", &small_comm_world);
   m.def("small_comm_ops", &small_comm_ops, "collectives issued on a handle so far");
   m.def("small_all_reduce_", &small_all_reduce_py, "in-place SUM on the current stream");
-  m.def("small_comm_kind", &small_comm_kind, "0 none, 1 RCCL, 2 xGMI, 3 emulated");
+  m.def("small_comm_kind", &small_comm_kind, "0 none, 1 RCCL, 2 xGMI, 3 emulated, 4 emulated fused xGMI");
   m.def("small_comm_rank", &small_comm_rank, "this process's rank on the communicator");
   m.def("small_all_gather", &small_all_gather, "rank-major all-gather along dim 0 (RCCL / emulated)");
   m.def("small_reduce_scatter", &small_reduce_scatter, "SUM reduce-scatter along dim 0 (RCCL / emulated)");

@@ -197,6 +197,16 @@ int& fold_add_pre() {
   return on;
 }
 
+// scoped fold_add_pre(): restored on every exit path, so an exception inside a folded
+// dgrad can never leave later dgrads on this thread in pre-rounding add mode
+struct AddPreScope {
+  int saved;
+  AddPreScope() : saved(fold_add_pre()) { fold_add_pre() = 1; }
+  ~AddPreScope() { fold_add_pre() = saved; }
+  AddPreScope(const AddPreScope&) = delete;
+  AddPreScope& operator=(const AddPreScope&) = delete;
+};
+
 torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                               int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
                               c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0,
@@ -480,16 +490,19 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
 // Ticket counters of the single-launch column reduction: zeroed once per device, reset by
 // each launch's last block; consecutive launches rotate through slots so launches on
 // different streams never share a counter.
-unsigned* reduce_counters(const torch::Device& dev) {
+// nslots consecutive slots: one per emulated rank of a fused SyncBN exchange (XgmiCol mode 2)
+unsigned* reduce_counters(const torch::Device& dev, int nslots) {
   constexpr int kSlots = 256, kPerSlot = 64;   // 64 column groups = 4096 channels
+  TORCH_CHECK(nslots >= 1 && nslots <= kXgmiMaxPeers, "counter slots");
   static std::mutex mu;
   static std::map<int, std::pair<torch::Tensor, int>> pool;
   std::lock_guard<std::mutex> lk(mu);
   auto& e = pool[dev.index()];
   if (!e.first.defined())
     e.first = torch::zeros({kSlots * kPerSlot}, torch::TensorOptions().dtype(at::kInt).device(dev));
-  const int slot = e.second;
-  e.second = (slot + 1) % kSlots;
+  int slot = e.second;
+  if (slot + nslots > kSlots) slot = 0;
+  e.second = (slot + nslots) % kSlots;
   return reinterpret_cast<unsigned*>(e.first.data_ptr<int>()) + slot * kPerSlot;
 }
 
@@ -500,8 +513,15 @@ void check_slab(const torch::Tensor& slab, int64_t nsets) {
   TORCH_CHECK(slab.size(2) <= 4096, "C <= 4096");
 }
 
-torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t nsets, int64_t C) {
-  return torch::empty({col_reduce_gy((int)rows) * nsets * C}, like.options().dtype(at::kDouble));
+torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t nsets, int64_t C, int z) {
+  return torch::empty({z * col_reduce_gy((int)rows) * nsets * C}, like.options().dtype(at::kDouble));
+}
+
+// the fused SyncBN exchange of one BN (xGMI communicators; csrc/kernels/bn.hip XgmiCol)
+FusedX fused_exchange(int64_t comm) {
+  FusedX f;
+  if (comm != 0) f.on = small_comm_fused(comm, &f.x);
+  return f;
 }
 
 namespace {
@@ -567,8 +587,11 @@ std::vector<torch::Tensor> bn_finalize(torch::Tensor sums, double count, OptT ga
 }
 
 // conv stat slab -> (scale, shift, mean, invstd) in ONE launch (no cross-rank reduction)
-std::vector<torch::Tensor> bn_stats_finalize(torch::Tensor slab, double count, OptT gamma, OptT beta, double eps,
-                                             double momentum, bool update, OptT running_mean, OptT running_var) {
+// fx (fused SyncBN exchange): the sums are exchanged across ranks inside the same launch
+// and `count` must be the global row count
+std::vector<torch::Tensor> bn_stats_finalize_x(torch::Tensor slab, double count, OptT gamma, OptT beta, double eps,
+                                               double momentum, bool update, OptT running_mean, OptT running_var,
+                                               const FusedX* fx) {
   check_slab(slab, 2);
   c10::DeviceGuard dg(slab.device());
   const int64_t rows = slab.size(0), C = slab.size(2);
@@ -576,11 +599,18 @@ std::vector<torch::Tensor> bn_stats_finalize(torch::Tensor slab, double count, O
   const BnFinalizeArgs a =
       finalize_args(slab, C, count, gamma, beta, eps, momentum, update, running_mean, running_var, o);
   auto sums = torch::empty({2, C}, slab.options().dtype(at::kDouble));
-  auto scratch = reduce_scratch(slab, rows, 2, C);
+  const int z = fx ? fx->z() : 1;
+  auto scratch = reduce_scratch(slab, rows, 2, C, z);
   check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, 2, C, scratch.data_ptr<double>(),
-                              reduce_counters(slab.device()), sums.data_ptr<double>(), 1, &a, nullptr, cur_stream()),
+                              reduce_counters(slab.device(), z), sums.data_ptr<double>(), 1, &a, nullptr, cur_stream(),
+                              fx ? fx->p() : nullptr),
             "bn_stats_finalize");
   return {o.scale, o.shift, o.mean, o.invstd};
+}
+
+std::vector<torch::Tensor> bn_stats_finalize(torch::Tensor slab, double count, OptT gamma, OptT beta, double eps,
+                                             double momentum, bool update, OptT running_mean, OptT running_var) {
+  return bn_stats_finalize_x(slab, count, gamma, beta, eps, momentum, update, running_mean, running_var, nullptr);
 }
 
 std::vector<torch::Tensor> bn_eval_affine(OptT gamma, OptT beta, torch::Tensor rm, torch::Tensor rv, double eps) {
@@ -772,27 +802,36 @@ std::vector<torch::Tensor> bn_bwd_coef(torch::Tensor sums, double count, OptT g_
 
 // bn_bwd_reduce + bn_bwd_coef in one elementwise launch + one reduction launch (no
 // cross-rank all-reduce of the sums in between)
-std::vector<torch::Tensor> bn_bwd_reduce_coef(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma,
-                                              OptT yb, OptT mb, OptT msc, OptT msh, double count, OptT g_a,
-                                              torch::Tensor inv_a, OptT g_b, OptT inv_b, OptT sink_ga, OptT sink_ba,
-                                              OptT sink_gb, OptT sink_bb) {
+std::vector<torch::Tensor> bn_bwd_reduce_coef_x(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma,
+                                                OptT yb, OptT mb, OptT msc, OptT msh, double count, OptT g_a,
+                                                torch::Tensor inv_a, OptT g_b, OptT inv_b, OptT sink_ga, OptT sink_ba,
+                                                OptT sink_gb, OptT sink_bb, const FusedX* fx, double grad_scale) {
   const BwdIn in = bwd_inputs(dout, outv, ya, ma, yb, mb, msc, msh);
   c10::DeviceGuard dg(dout.device());
   const int64_t C = in.C;
   const int nsum = in.ybp ? 3 : 2;
   CoefOut o;
   const BnCoefArgs a = coef_args(dout, C, nsum - 1, count, g_a, ma, inv_a, g_b, mb, inv_b, sink_ga, sink_ba, sink_gb,
-                                 sink_bb, o);
+                                 sink_bb, o, grad_scale);
   const int g = bn_bwd_reduce_blocks(dout.numel(), C);
+  const int z = fx ? fx->z() : 1;
   auto sums = torch::empty({nsum, C}, dout.options().dtype(at::kDouble));
   auto partial = torch::empty({g, nsum, C}, dout.options().dtype(at::kFloat));
-  auto scratch = reduce_scratch(dout, g, nsum, C);
+  auto scratch = reduce_scratch(dout, g, nsum, C, z);
   check_hip(launch_bn_bwd_reduce(dout.data_ptr(), in.op, ya.data_ptr(), ma.data_ptr<float>(), in.ybp, in.mbp,
                                  dout.numel(), C, partial.data_ptr<float>(), scratch.data_ptr<double>(),
-                                 reduce_counters(dout.device()), sums.data_ptr<double>(), 2, &a, cur_stream(),
-                                 in.mk_s, in.mk_t, in.om),
+                                 reduce_counters(dout.device(), z), sums.data_ptr<double>(), 2, &a, cur_stream(),
+                                 in.mk_s, in.mk_t, in.om, fx ? fx->p() : nullptr),
             "bn_bwd_reduce_coef");
   return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
+}
+
+std::vector<torch::Tensor> bn_bwd_reduce_coef(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ma,
+                                              OptT yb, OptT mb, OptT msc, OptT msh, double count, OptT g_a,
+                                              torch::Tensor inv_a, OptT g_b, OptT inv_b, OptT sink_ga, OptT sink_ba,
+                                              OptT sink_gb, OptT sink_bb) {
+  return bn_bwd_reduce_coef_x(dout, outv, ya, ma, yb, mb, msc, msh, count, g_a, inv_a, g_b, inv_b, sink_ga, sink_ba,
+                              sink_gb, sink_bb, nullptr, 1.0);
 }
 
 std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dout, OptT outv, torch::Tensor ya, torch::Tensor ca, OptT yb,
@@ -863,6 +902,12 @@ BnState bn_forward(const torch::Tensor& slab, double count, const torch::Tensor&
                    int64_t comm) {
   if (training) {
     if (comm != 0 && small_comm_world(comm) > 1) {
+      const FusedX fx = fused_exchange(comm);
+      if (fx.on) {   // reduce + exchange + finalize: one launch
+        auto r = bn_stats_finalize_x(slab, count * small_comm_world(comm), g, b, eps, mom, true, rm, rv, &fx);
+        small_comm_fused_issued(comm);
+        return {r[0], r[1], r[2], r[3]};
+      }
       auto sums = bn_stats_reduce(slab);
       small_all_reduce_(comm, sums);
       auto r = bn_finalize(sums, count * small_comm_world(comm), g, b, eps, mom, true, rm, rv);
@@ -914,9 +959,16 @@ std::vector<torch::Tensor> bn_bwd_sync(int64_t comm, torch::Tensor dout, OptT ou
   if (comm == 0 || small_comm_world(comm) == 1)
     return bn_bwd_reduce_coef(dout, outv, ya, ma, yb, mb, msc, msh, count, g_a, inv_a, g_b, inv_b, sink_ga, sink_ba,
                               sink_gb, sink_bb);
+  const int w = small_comm_world(comm);
+  const FusedX fx = fused_exchange(comm);
+  if (fx.on) {
+    auto r = bn_bwd_reduce_coef_x(dout, outv, ya, ma, yb, mb, msc, msh, count * w, g_a, inv_a, g_b, inv_b, sink_ga,
+                                  sink_ba, sink_gb, sink_bb, &fx, 1.0 / w);
+    small_comm_fused_issued(comm);
+    return r;
+  }
   auto sums = bn_bwd_reduce(dout, outv, ya, ma, yb, mb, msc, msh);
   small_all_reduce_(comm, sums);
-  const int w = small_comm_world(comm);
   return bn_bwd_coef(sums, count * w, g_a, ma, inv_a, g_b, mb, inv_b, sink_ga, sink_ba, sink_gb, sink_bb, 1.0 / w);
 }
 
@@ -946,6 +998,20 @@ std::vector<torch::Tensor> bn_bwd_coef_slab(int64_t comm, torch::Tensor slab, do
   c10::DeviceGuard dg(slab.device());
   const int64_t rows = slab.size(0), nsum = slab.size(1), C = slab.size(2);
   auto sums = torch::empty({nsum, C}, slab.options().dtype(at::kDouble));
+  const FusedX fx = fused_exchange(comm);
+  if (fx.on) {   // reduce + exchange + coefficients: one launch (global count, this rank's 1/W of dγ/dβ)
+    const int w = small_comm_world(comm);
+    CoefOut o;
+    const BnCoefArgs a = coef_args(slab, C, (int)nsum - 1, count * w, g_a, mean_a, inv_a, g_b, mean_b, inv_b,
+                                   sink_ga, sink_ba, sink_gb, sink_bb, o, 1.0 / w);
+    auto scratch = reduce_scratch(slab, rows, nsum, C, fx.z());
+    check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, (int)nsum, C, scratch.data_ptr<double>(),
+                                reduce_counters(slab.device(), fx.z()), sums.data_ptr<double>(), 2, nullptr, &a,
+                                cur_stream(), fx.p()),
+              "bn_bwd_coef_slab(fused exchange)");
+    small_comm_fused_issued(comm);
+    return {o.coef_a, o.coef_b, o.dga, o.dba, o.dgb, o.dbb};
+  }
   auto scratch = reduce_scratch(slab, rows, nsum, C);
   if (comm != 0 && small_comm_world(comm) > 1) {
     check_hip(launch_col_reduce(slab.data_ptr<float>(), rows, (int)nsum, C, scratch.data_ptr<double>(),
@@ -1304,9 +1370,8 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
       // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
       auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2, S(lastbn, 2), gram3);
       side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3);
-      fold_add_pre() = 1;
+      AddPreScope pre;
       r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
-      fold_add_pre() = 0;
     } else {
       side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
       r2 = dgrad_bn(dylast, wt[2], y2, 1, 0, 1, cnt_last);
@@ -1345,9 +1410,10 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
     auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x, S(nconv, 2), grams_sc);
     side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side, grams_sc);
-    fold_add_pre() = 1;
-    dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
-    fold_add_pre() = 0;
+    {
+      AddPreScope pre;
+      dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
+    }
     dx = last_dgrad(dx, dx, c10::nullopt);
   } else if (proj) {
     side_wgrad(dys, x, 1, 1, stride, 0, dw[nconv], side);
@@ -1370,9 +1436,40 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   return {dx, prev_slab};
 }
 
+// Column reduction + cross-rank exchange of a statistics slab in ONE launch (the fused
+// SyncBN path without an epilogue): tests, the start-up self-check of an xGMI communicator
+// and the per-BN latency probe (tools/syncbn_latency.py). Real communicator: slab
+// [rows][nsets][C] -> global sums [nsets][C]. Emulated (XEMU): slab [W][rows][nsets][C],
+// virtual rank z reduces slab[z], or [rows][nsets][C] shared by identical ranks; rank 0's
+// global sums are returned.
+torch::Tensor syncbn_exchange_sums(int64_t comm, torch::Tensor slab) {
+  FusedX fx = fused_exchange(comm);
+  TORCH_CHECK(fx.on, "syncbn_exchange_sums: not a fused (xGMI) communicator of > 1 ranks");
+  TORCH_CHECK(slab.is_cuda() && slab.scalar_type() == at::kFloat && slab.is_contiguous(), "slab: contiguous fp32");
+  const bool emu = fx.x.mode == 2;
+  // emulated ranks: [W][rows][nsets][C] (rank z reduces slab[z]) or [rows][nsets][C] (identical ranks)
+  TORCH_CHECK(slab.dim() == 3 || (emu && slab.dim() == 4), "slab: [rows][nsets][C]",
+              emu ? " or [W][rows][nsets][C]" : "");
+  if (slab.dim() == 4) TORCH_CHECK(slab.size(0) == fx.x.world, "slab: one block per emulated rank");
+  const int64_t rows = slab.size(-3), nsets = slab.size(-2), C = slab.size(-1);
+  TORCH_CHECK(nsets >= 1 && nsets <= 3 && C >= 1 && C <= 4096 && rows >= 1, "slab shape");
+  if (slab.dim() == 4) fx.x.slab_zstride = (long)(rows * nsets * C);
+  c10::DeviceGuard dg(slab.device());
+  auto sums = torch::empty({nsets, C}, slab.options().dtype(at::kDouble));
+  auto scratch = reduce_scratch(slab, rows, nsets, C, fx.z());
+  check_hip(launch_col_reduce(slab.data_ptr<float>(), (int)rows, (int)nsets, (int)C, scratch.data_ptr<double>(),
+                              reduce_counters(slab.device(), fx.z()), sums.data_ptr<double>(), 0, nullptr, nullptr,
+                              cur_stream(), fx.p()),
+            "syncbn_exchange_sums");
+  small_comm_fused_issued(comm);
+  return sums;
+}
+
 }  // namespace
 
 void register_conv_bn(pybind11::module& m) {
+  m.def("syncbn_exchange_sums", &syncbn_exchange_sums,
+        "column reduction + cross-rank exchange of a BN statistics slab in one launch (fused xGMI communicators)");
   m.def("stat_fuse_set", &stat_fuse_set,
         "in-kernel BN-statistics reduction of the block executor (bits: 1 forward, 2 backward); returns the "
         "previous bits",

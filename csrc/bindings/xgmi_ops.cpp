@@ -12,6 +12,7 @@ namespace sdx_bind {
 namespace {
 
 struct Arena {
+  bool emulated = false;           // W virtual ranks' arenas in this device's memory (tests)
   int device = 0;
   int rank = 0;
   int world = 1;
@@ -29,7 +30,9 @@ std::vector<std::unique_ptr<Arena>> g_arenas;
 
 size_t arena_bytes(int world, size_t cap) {
   const size_t data = 2ull * world * cap * sizeof(double);
-  return data + 256;   // flags [2][W] u32 (≤ 64 B) after the data, 256-B aligned block
+  // flags [2][W][kXgmiFlagGroups] u32 after the data (≤ 4 KiB), 256-B aligned block
+  const size_t flags = 2ull * world * kXgmiFlagGroups * sizeof(unsigned);
+  return data + (flags + 255) / 256 * 256;
 }
 
 Arena& get(int64_t id) {
@@ -128,6 +131,33 @@ void xgmi_destroy(int64_t id) {
   (void)hipHostFree(a->err);
 }
 
+// W virtual ranks on this device (single-GPU emulation of the fused SyncBN exchange, the
+// XEMU small-communicator kind): W arenas in one ordinary device allocation (agent scope),
+// error word host-pinned like a real arena's so the watchdog reads it the same way
+int64_t xgmi_emu_create(int64_t world, int64_t cap, double timeout_s) {
+  TORCH_CHECK(world >= 1 && world <= kXgmiMaxPeers, "1 <= world <= 8");
+  TORCH_CHECK(cap > 0 && cap <= (1 << 20), "cap in (0, 2^20]");
+  auto a = std::make_unique<Arena>();
+  a->emulated = true;
+  check_hip(hipGetDevice(&a->device), "hipGetDevice");
+  a->world = (int)world;
+  a->cap = (size_t)cap;
+  const size_t one = arena_bytes(a->world, a->cap);
+  check_hip(hipMalloc(&a->base, one * world), "hipMalloc(emulated arenas)");
+  check_hip(hipMemset(a->base, 0, one * world), "hipMemset");
+  a->peers.cap = a->cap;
+  for (int q = 0; q < a->world; ++q) set_ptrs(a->peers, q, static_cast<char*>(a->base) + one * q, a->world, a->cap);
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&a->err), sizeof(int), hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(err)");
+  *reinterpret_cast<volatile int*>(a->err) = 0;
+  int rate_khz = 0;
+  check_hip(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, a->device), "wall clock rate");
+  a->timeout_ticks = (long long)(timeout_s * 1000.0 * (rate_khz > 0 ? rate_khz : 100000));
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_arenas.push_back(std::move(a));
+  return (int64_t)g_arenas.size() - 1;
+}
+
 // W virtual ranks on this GPU: `in` [W, n] fp64; runs `iters` calls (epochs 1..iters, so both
 // parities and arena reuse are exercised) and returns the last result [W, n].
 torch::Tensor xgmi_emulate(torch::Tensor in, int64_t iters) {
@@ -159,10 +189,35 @@ torch::Tensor xgmi_emulate(torch::Tensor in, int64_t iters) {
 
 }  // namespace
 
+// for comm_ops.cpp / conv_bn_ops.cpp: arguments of one fused SyncBN exchange on arena id
+// (epoch advanced; mode 1 real peers, 2 emulated ranks)
+XgmiCol xgmi_col_args(int64_t id) {
+  Arena& a = get(id);
+  XgmiCol x{};
+  x.peers = a.peers;
+  x.mode = a.emulated ? 2 : 1;
+  x.me = a.rank;
+  x.world = a.world;
+  x.epoch = ++a.epoch;
+  x.err = a.err;
+  x.timeout_ticks = a.timeout_ticks;
+  x.slab_zstride = 0;
+  return x;
+}
+bool xgmi_emulated(int64_t id) { return get(id).emulated; }
+int64_t xgmi_emu_create_ext(int64_t world, int64_t cap, double timeout_s) { return xgmi_emu_create(world, cap, timeout_s); }
+
 // for comm_ops.cpp (small-communicator wrapper of an arena)
 torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x) { return xgmi_allreduce(id, x); }
 int64_t xgmi_world(int64_t id) { return get(id).world; }
 int64_t xgmi_error_ext(int64_t id) { return xgmi_error(id); }
+// watchdog sweep: never throws; 0 once the arena is gone (the read happens under the
+// registry lock, and xgmi_destroy unlinks an arena under that lock before freeing it)
+int64_t xgmi_error_nothrow(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (id < 0 || id >= (int64_t)g_arenas.size() || !g_arenas[id]) return 0;
+  return *reinterpret_cast<volatile int*>(g_arenas[id]->err);
+}
 std::vector<int64_t> xgmi_debug(int64_t id) {
   Arena& a = get(id);
   return {(int64_t)(uintptr_t)a.err, (int64_t)*reinterpret_cast<volatile int*>(a.err), (int64_t)a.world};
@@ -178,6 +233,8 @@ void register_xgmi(pybind11::module& m) {
   m.def("xgmi_destroy", &xgmi_destroy);
   m.def("xgmi_debug", &xgmi_debug);
   m.def("xgmi_emulate", &xgmi_emulate, "single-GPU W-rank emulation of the one-shot protocol");
+  m.def("xgmi_emu_create", &xgmi_emu_create, "W emulated ranks' arenas on this device (fused SyncBN exchange tests)",
+        pybind11::arg("world"), pybind11::arg("cap") = 12288, pybind11::arg("timeout_s") = 10.0);
 }
 
 }  // namespace sdx_bind

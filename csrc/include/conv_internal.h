@@ -3,6 +3,8 @@
 #pragma once
 #include <torch/extension.h>
 
+#include "launchers.h"
+
 namespace sdx_bind {
 using OptT = c10::optional<torch::Tensor>;
 
@@ -15,6 +17,15 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim = 0, bool fill = false);
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                          int64_t splits, int64_t cfg, OptT out, bool accumulate, OptT in_scale, OptT in_shift);
 // ticket counters + fp64 scratch of the single-launch column reduction (bn.hip col_reduce)
-unsigned* reduce_counters(const torch::Device& dev);
-torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t nsets, int64_t C);
+// (nslots / z: one block per emulated rank of a fused SyncBN exchange, XgmiCol mode 2)
+unsigned* reduce_counters(const torch::Device& dev, int nslots = 1);
+torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t nsets, int64_t C, int z = 1);
+// the fused SyncBN exchange of one BN on communicator `comm` (off: reduce -> all-reduce -> epilogue)
+struct FusedX {
+  XgmiCol x{};
+  bool on = false;
+  int z() const { return on && x.mode == 2 ? x.world : 1; }
+  const XgmiCol* p() const { return on ? &x : nullptr; }
+};
+FusedX fused_exchange(int64_t comm);
 }  // namespace sdx_bind

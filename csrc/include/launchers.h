@@ -162,13 +162,43 @@ struct StatFuse {
   BnCoefArgs ca;
 };
 
+// ---- xGMI peer arenas (xgmi.hip, bn.hip) ----------------------------------------------
+constexpr int kXgmiMaxPeers = 8;
+constexpr int kXgmiFlagGroups = 64;   // per-sender flags per parity: one per 64-channel column group
+struct XgmiPeers {
+  double* data[kXgmiMaxPeers];     // each rank's receive arena: [2][W][cap] fp64 (IPC-mapped)
+  unsigned* flags[kXgmiMaxPeers];  // each rank's flags: [2][W][kXgmiFlagGroups] u32
+  size_t cap;                      // elements per slot
+};
+// SyncBN statistics exchanged INSIDE the column reduction (bn.hip): the last block of
+// every 64-channel group stores its [nsets][64] fp64 sums into every rank's arena slot
+// [parity][me], publishes the group's flag, waits for every sender's flag of that group
+// and sums the W slots in rank order (bit-identical on every rank) before its epilogue —
+// reduce + all-reduce + finalize/coefficients in ONE launch.
+//   mode 1: real peers (IPC-mapped uncached arenas, system scope).
+//   mode 2: single-GPU emulation — `world` virtual ranks are gridDim.z of the SAME launch
+//           (arenas in device memory, agent scope); rank z reduces slab + z·slab_zstride
+//           (0: identical ranks, the EMU semantics Σ = W·x) and only rank 0 writes the sums
+//           and runs the epilogue. counters/scratch are W consecutive per-rank blocks.
+struct XgmiCol {
+  XgmiPeers peers;
+  int mode = 0, me = 0, world = 1;
+  unsigned epoch = 0;
+  int* err = nullptr;               // host-pinned: 1 + sender whose flag missed the deadline
+  long long timeout_ticks = 0;      // 100 MHz wall-clock ticks
+  long slab_zstride = 0;            // mode 2: elements between virtual ranks' slabs
+};
+
 // Deterministic reduction of a [rows][nsets][C] fp32 slab to fp64 sums [nsets][C] in ONE
 // launch (per-block partials + last-arriver combine; no memset). epi: 0 sums only,
 // 1 + BN finalize (nsets 2), 2 + BN backward coefficients (nsets 2|3), 3 gradient-sink add
 // of set 0 (ca->dbeta_a[c] += Σ·ca->grad_scale: a bias gradient; nsets 1|2).
 int col_reduce_gy(int rows);
+// xg (optional): cross-rank exchange of the sums before the epilogue (see XgmiCol); the
+// epilogue's count must then be the global row count
 hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, double* scratch, unsigned* counters,
-                             double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s);
+                             double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s,
+                             const XgmiCol* xg = nullptr);
 hipError_t launch_bn_finalize(const double* sums, int C, const BnFinalizeArgs& a, hipStream_t s);
 hipError_t launch_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                                  float eps, float* scale, float* shift, hipStream_t s);
@@ -181,7 +211,8 @@ int bn_bwd_reduce_blocks(long numel, int C);
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
                                 const float* mb, long numel, int C, float* partial, double* scratch,
                                 unsigned* counters, double* sums, int epi, const BnCoefArgs* ca, hipStream_t s,
-                                const float* msc = nullptr, const float* msh = nullptr, const void* omask = nullptr);
+                                const float* msc = nullptr, const float* msh = nullptr, const void* omask = nullptr,
+                                const XgmiCol* xg = nullptr);
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, const BnCoefArgs& a, hipStream_t s);
 hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* ya, const float* ca, const void* yb,
                                const float* cb, void* dya, void* dyb, void* dz_out, long numel, int C, hipStream_t s,
@@ -215,12 +246,6 @@ hipError_t launch_gap_bwd(const float* dy, void* dx, int N, int HW, int C, hipSt
 hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s);
 
 // ---- one-shot small all-reduce over xGMI peer memory (xgmi.hip) --------------------
-constexpr int kXgmiMaxPeers = 8;
-struct XgmiPeers {
-  double* data[kXgmiMaxPeers];     // each rank's receive arena: [2][W][cap] fp64 (IPC-mapped)
-  unsigned* flags[kXgmiMaxPeers];  // each rank's flags: [2][W] u32
-  size_t cap;                      // elements per slot
-};
 // err: host-pinned int (1 + rank of a peer whose flag missed the deadline of timeout_ticks
 // of the 100 MHz wall clock; the sum is then skipped)
 hipError_t launch_xgmi_allreduce(const double* in, double* out, int n, const XgmiPeers& peers, int me, int world,

@@ -34,13 +34,85 @@ namespace {
 // with write-through (sc1) stores and read back with sc1 loads, so no agent-scope release
 // fence is needed: such a fence would write back the whole L2 (still dirty with the
 // producing conv's output) in every block.
-template <int NS, int EPI>
+//
+// XG != 0: SyncBN exchange before the epilogue (launchers.h XgmiCol). The last block of
+// group x stores its [NS][64] sums into slot [parity][me] of every rank's arena with
+// write-through (system scope: the arenas are uncached, IPC-mapped peer memory; agent
+// scope for the single-GPU emulation) stores, drains them (s_waitcnt vmcnt(0): the
+// stores are acknowledged), publishes the epoch in flag [parity][me][x] of every arena,
+// and polls its own W flags of group x against the wall-clock deadline. The slots are
+// then summed in rank order, so every rank holds bit-identical global sums, and the
+// epilogue (finalize / coefficients, with the global count) runs on them. Every 64-channel
+// group is an independent instance of the two-parity protocol of xgmi.hip, and no block
+// waits on another block of its own launch, so the kernel cannot deadlock on itself.
+template <int NS, int XG>
+__device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, int me) {
+  constexpr int kScope = XG == 1 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
+  const int W = xg.world;
+  const int par = xg.epoch & 1;
+  const size_t cap = xg.peers.cap;
+  __shared__ int ok;
+  if (threadIdx.x < 64 && c < C) {
+    for (int p = 0; p < W; ++p) {
+      unsigned long long* dst =
+          reinterpret_cast<unsigned long long*>(xg.peers.data[p] + ((size_t)par * W + me) * cap);
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+        __hip_atomic_store(dst + (size_t)q * C + c, (unsigned long long)__double_as_longlong(t[q]), __ATOMIC_RELAXED,
+                           kScope);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's data stores are acknowledged
+  if (threadIdx.x == 0) ok = 1;
+  __syncthreads();
+  if (threadIdx.x < W) {   // wave 0: the same wave that stored the data, after its drain
+    const int p = threadIdx.x;
+    __hip_atomic_store(xg.peers.flags[p] + ((size_t)par * W + me) * kXgmiFlagGroups + blockIdx.x, xg.epoch,
+                       __ATOMIC_RELAXED, kScope);
+    unsigned* f = xg.peers.flags[me] + ((size_t)par * W + p) * kXgmiFlagGroups + blockIdx.x;
+    const long long t0 = wall_clock64();
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, kScope) != xg.epoch) {
+      if ((++spins & 63) == 0 && wall_clock64() - t0 > xg.timeout_ticks) {
+        atomicExch(&ok, 0);
+        if (xg.err) __hip_atomic_store(xg.err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (!ok) return false;
+  if (threadIdx.x < 64 && c < C) {
+    const unsigned long long* base =
+        reinterpret_cast<const unsigned long long*>(xg.peers.data[me] + (size_t)par * W * cap);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      double v = 0.0;
+      for (int p = 0; p < W; ++p)
+        v += __longlong_as_double(
+            (long long)__hip_atomic_load(base + (size_t)p * cap + (size_t)q * C + c, __ATOMIC_RELAXED, kScope));
+      t[q] = v;
+    }
+  }
+  return true;
+}
+
+template <int NS, int EPI, int XG>
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ slab, int rows, int C,
                                                          double* scratch, unsigned* counters,
-                                                         double* __restrict__ sums, BnFinalizeArgs fa, BnCoefArgs ca) {
+                                                         double* __restrict__ sums, BnFinalizeArgs fa, BnCoefArgs ca,
+                                                         XgmiCol xg) {
   __shared__ double red[NS][4][64];
   __shared__ int is_last;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  // emulated ranks (XG == 2): virtual rank z = blockIdx.z has its own slab, scratch and counters
+  const int vz = XG == 2 ? (int)blockIdx.z : 0;
+  if constexpr (XG == 2) {
+    slab += (size_t)vz * xg.slab_zstride;
+    scratch += (size_t)vz * gridDim.y * NS * C;
+    counters += vz * 64;
+  }
   const int c = blockIdx.x * 64 + tx;
   const int gy = gridDim.y;
   const int per = (rows + gy - 1) / gy;
@@ -118,10 +190,12 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
     for (int q = 0; q < NS; ++q) red[q][ty][tx] = t[q];
     __syncthreads();
   }
-  if (ty == 0 && c < C) {
-    double t[NS];
+  double t[NS];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) t[q] = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
+  for (int q = 0; q < NS; ++q) t[q] = red[q][0][tx] + red[q][1][tx] + red[q][2][tx] + red[q][3][tx];
+  bool go = true;
+  if constexpr (XG != 0) go = xg_exchange<NS, XG>(t, c, C, xg, XG == 2 ? vz : xg.me);
+  if (go && ty == 0 && c < C && vz == 0) {
 #pragma unroll
     for (int q = 0; q < NS; ++q) sums[(size_t)q * C + c] = t[q];
     if constexpr (EPI == 1) bn_finalize_one(c, t[0], t[1], fa);
@@ -479,14 +553,32 @@ int col_reduce_gy(int rows) {
 }
 
 hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, double* scratch, unsigned* counters,
-                             double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s) {
+                             double* sums, int epi, const BnFinalizeArgs* fa, const BnCoefArgs* ca, hipStream_t s,
+                             const XgmiCol* xg) {
   if (rows < 1 || C < 1 || (epi == 1 && (nsets != 2 || !fa)) || (epi == 2 && (nsets < 2 || !ca)) ||
       (epi == 3 && (nsets > 2 || !ca || !ca->dbeta_a)) || (nsets == 1 && epi != 0 && epi != 3))
     return hipErrorInvalidValue;
-  const dim3 grid((C + 63) / 64, col_reduce_gy(rows)), blk(256);
+  const int xm = xg ? xg->mode : 0;
+  if (xg && (xm < 1 || xm > 2 || xg->world < 1 || xg->world > kXgmiMaxPeers || xg->me < 0 || xg->me >= xg->world ||
+             (size_t)nsets * C > xg->peers.cap || (C + 63) / 64 > kXgmiFlagGroups || xg->timeout_ticks <= 0))
+    return hipErrorInvalidValue;
+  if (xg && xm == 2 && xg->slab_zstride < 0) return hipErrorInvalidValue;
+  const dim3 grid((C + 63) / 64, col_reduce_gy(rows), xm == 2 ? xg->world : 1), blk(256);
   const BnFinalizeArgs f = fa ? *fa : BnFinalizeArgs{};
   const BnCoefArgs k = ca ? *ca : BnCoefArgs{};
-#define SDX_CR(NS, EPI) hipLaunchKernelGGL((col_reduce_kernel<NS, EPI>), grid, blk, 0, s, slab, rows, C, scratch, counters, sums, f, k)
+  const XgmiCol x = xg ? *xg : XgmiCol{};
+#define SDX_CR(NS, EPI)                                                                                              \
+  do {                                                                                                               \
+    if (xm == 0)                                                                                                     \
+      hipLaunchKernelGGL((col_reduce_kernel<NS, EPI, 0>), grid, blk, 0, s, slab, rows, C, scratch, counters, sums, f, \
+                         k, x);                                                                                      \
+    else if (xm == 1)                                                                                                \
+      hipLaunchKernelGGL((col_reduce_kernel<NS, EPI, 1>), grid, blk, 0, s, slab, rows, C, scratch, counters, sums, f, \
+                         k, x);                                                                                      \
+    else                                                                                                             \
+      hipLaunchKernelGGL((col_reduce_kernel<NS, EPI, 2>), grid, blk, 0, s, slab, rows, C, scratch, counters, sums, f, \
+                         k, x);                                                                                      \
+  } while (0)
   if (nsets == 1) {
     if (epi == 0) SDX_CR(1, 0); else SDX_CR(1, 3);
   } else if (nsets == 2) {
@@ -546,7 +638,7 @@ int bn_bwd_reduce_blocks(long numel, int C) {
 hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* ya, const float* ma, const void* yb,
                                 const float* mb, long numel, int C, float* partial, double* scratch,
                                 unsigned* counters, double* sums, int epi, const BnCoefArgs* ca, hipStream_t s,
-                                const float* msc, const float* msh, const void* omask) {
+                                const float* msc, const float* msh, const void* omask, const XgmiCol* xg) {
   const int nsets = yb ? 3 : 2;
   const long n8 = numel / 8;
   const int C8 = C / 8;
@@ -561,7 +653,9 @@ hipError_t launch_bn_bwd_reduce(const void* dout, const void* outv, const void* 
                        (const uint16_t*)outv, (const uint16_t*)ya, ma, (const uint16_t*)nullptr, (const float*)nullptr,
                        n8, C8, C, partial, msc, msh, (const uint8_t*)omask);
   SDX_LAUNCH_CHECK();
-  return launch_col_reduce(partial, g, nsets, C, scratch, counters, sums, epi, nullptr, ca, s);
+  // emulated ranks (xg mode 2) all reduce the same partial slab (identical ranks)
+  if (xg && xg->mode == 2 && xg->slab_zstride != 0) return hipErrorInvalidValue;
+  return launch_col_reduce(partial, g, nsets, C, scratch, counters, sums, epi, nullptr, ca, s, xg);
 }
 
 hipError_t launch_bn_bwd_coef(const double* sums, int nsets, int C, const BnCoefArgs& a, hipStream_t s) {

@@ -3,7 +3,10 @@
 // the critical path; a ring collective pays 2(W−1) link latencies for each of them).
 //
 // Every rank owns an IPC-shared receive arena in uncached device memory:
-//   data [2 parity][W senders][cap] fp64,   flags [2 parity][W senders] u32.
+//   data [2 parity][W senders][cap] fp64,   flags [2 parity][W senders][64 groups] u32
+//   (this kernel uses group 0; the SyncBN column reduction of bn.hip one flag per
+//   64-channel group — every call uses group 0, so the parity argument below holds for
+//   any mix of the two).
 // A call with epoch e (host counter, starting at 1) and parity e&1:
 //   1. each rank stores its n values straight into slot [parity][me] of EVERY rank's arena
 //      (remote stores travel over the point-to-point xGMI link to that peer);
@@ -47,10 +50,10 @@ __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__
   if (threadIdx.x < world) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (SCOPE == 1)
-      __hip_atomic_store(peers.flags[threadIdx.x] + par * world + me, epoch, __ATOMIC_RELEASE,
+      __hip_atomic_store(peers.flags[threadIdx.x] + (par * world + me) * kXgmiFlagGroups, epoch, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     else
-      __hip_atomic_store(peers.flags[threadIdx.x] + par * world + me, epoch, __ATOMIC_RELEASE,
+      __hip_atomic_store(peers.flags[threadIdx.x] + (par * world + me) * kXgmiFlagGroups, epoch, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
   // 3. wait for every sender's flag in my arena
@@ -58,7 +61,7 @@ __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__
   if (threadIdx.x == 0) ok_all = 1;
   __syncthreads();
   if (threadIdx.x < world) {
-    unsigned* f = peers.flags[me] + par * world + threadIdx.x;
+    unsigned* f = peers.flags[me] + (par * world + threadIdx.x) * kXgmiFlagGroups;
     const long long t0 = wall_clock64();
     unsigned spins = 0;
     while (true) {

@@ -120,15 +120,34 @@ def synthetic_dataset(n: int = 50000, size: int = 32, num_classes: int = 10, see
     return ArrayDataset(imgs, labels, num_classes, "synthetic")
 
 
-def load_image_folder(root: str, size: Optional[int] = None, workers: int = 1) -> ArrayDataset:
+def ragged_side_cap(size: int, min_scale: float = 0.2, min_ratio: float = 3 / 4) -> int:
+    """Shorter-side bound for the native-resolution store: RandomResizedCrop's smallest box
+    (area ``min_scale``·H·W at aspect ``min_ratio``) still spans ``size`` source pixels
+    when the shorter side is at most ``size / sqrt(min_scale·min_ratio)`` (≈2.58·size), so
+    keeping more pixels than that adds bytes but no detail to any crop."""
+    import math
+    return int(math.ceil(size / math.sqrt(min_scale * min_ratio)))
+
+
+DATA_BUDGET_BYTES = int(float(os.environ.get("SDX_DATA_BUDGET_GB", "64")) * (1 << 30))
+
+
+def load_image_folder(root: str, size: Optional[int] = None, workers: int = 1, max_side: Optional[int] = None,
+                      budget_bytes: Optional[int] = None, dense_size: Optional[int] = None) -> ArrayDataset:
     """ImageFolder (class-per-subdirectory) decoded with PIL into uint8 RGB.
 
-    ``size=None`` (pretraining): every image is kept at its NATIVE resolution in a ragged
+    ``size=None`` (pretraining): images are kept near their NATIVE resolution in a ragged
     byte store (offsets + sizes), so the GPU RandomResizedCrop samples its box from the
-    original pixels exactly as torchvision does on the decoded image (main_supcon.py:170-
-    191); ``size=s``: resized to s x s into a dense [N, s, s, 3] array. Decoding runs on
-    ``workers`` threads (``--num_workers``; PIL releases the GIL while decoding).
+    original pixels as torchvision does on the decoded image (main_supcon.py:170-191).
+    The shorter side is capped at ``max_side`` (aspect kept; see :func:`ragged_side_cap`),
+    the sizes are read from the headers first and the flat store is preallocated and
+    filled in place (no second copy). If the store would exceed ``budget_bytes`` (default
+    ``SDX_DATA_BUDGET_GB``, 64 GiB: it lives in HBM next to training) the dense
+    ``dense_size``-resized store is built instead. ``size=s``: resized to s x s into a
+    dense [N, s, s, 3] array. Decoding runs on ``workers`` threads (``--num_workers``; PIL
+    releases the GIL while decoding).
     """
+    import logging
     from concurrent.futures import ThreadPoolExecutor
 
     from PIL import Image
@@ -144,24 +163,56 @@ def load_image_folder(root: str, size: Optional[int] = None, workers: int = 1) -
                     ys.append(ci)
     if not files:
         raise FileNotFoundError(f"no images under {root!r}")
-
-    def decode(path):
-        with Image.open(path) as im:
-            im = im.convert("RGB")
-            if size is not None:
-                im = im.resize((size, size), Image.BILINEAR)
-            return np.asarray(im, dtype=np.uint8)
-
-    with ThreadPoolExecutor(max_workers=max(1, int(workers))) as ex:
-        xs = list(ex.map(decode, files))
     labels = np.asarray(ys, dtype=np.int64)
     name = os.path.basename(os.path.normpath(root))
+    nw = max(1, int(workers))
+
+    def decode(path, hw=None):
+        with Image.open(path) as im:
+            im = im.convert("RGB")
+            if hw is not None and (im.height, im.width) != hw:
+                im = im.resize((hw[1], hw[0]), Image.BILINEAR)
+            return np.asarray(im, dtype=np.uint8)
+
+    def dense(s):
+        out = np.empty((len(files), s, s, 3), dtype=np.uint8)
+
+        def fill(i):
+            out[i] = decode(files[i], (s, s))
+        with ThreadPoolExecutor(max_workers=nw) as ex:
+            list(ex.map(fill, range(len(files))))
+        return ArrayDataset(out, labels, len(classes), name)
+
     if size is not None:
-        return ArrayDataset(np.stack(xs), labels, len(classes), name)
-    sizes = np.asarray([x.shape[:2] for x in xs], dtype=np.int32)
+        return dense(size)
+
+    def header(path):
+        with Image.open(path) as im:          # lazy: reads the header only
+            w, h = im.size
+        if max_side is not None and min(h, w) > max_side:
+            f = max_side / min(h, w)
+            h, w = max(1, round(h * f)), max(1, round(w * f))
+        return h, w
+
+    with ThreadPoolExecutor(max_workers=nw) as ex:
+        sizes = np.asarray(list(ex.map(header, files)), dtype=np.int32).reshape(-1, 2)
     nbytes = sizes[:, 0].astype(np.int64) * sizes[:, 1] * 3
+    total = int(nbytes.sum())
+    budget = DATA_BUDGET_BYTES if budget_bytes is None else int(budget_bytes)
+    if total > budget:
+        s = dense_size or (max_side or 256)
+        logging.warning(f"native-resolution store of {root!r} needs {total / 2**30:.1f} GiB > budget "
+                        f"{budget / 2**30:.1f} GiB: using a dense {s}x{s} store")
+        return dense(s)
     offsets = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.int64)
-    flat = np.concatenate([x.reshape(-1) for x in xs])
+    flat = np.empty(total, dtype=np.uint8)
+
+    def fill_ragged(i):
+        h, w = (int(v) for v in sizes[i])
+        o = int(offsets[i])
+        flat[o:o + h * w * 3] = decode(files[i], (h, w)).reshape(-1)
+    with ThreadPoolExecutor(max_workers=nw) as ex:
+        list(ex.map(fill_ragged, range(len(files))))
     return ArrayDataset(flat, labels, len(classes), name, offsets=offsets, sizes=sizes)
 
 
@@ -177,5 +228,7 @@ def build_dataset(dataset: str, data_folder: str, train: bool = True, synthetic:
     if dataset in _CIFAR:
         return load_cifar(dataset, data_folder, train)
     if dataset == "path":
-        return load_image_folder(data_folder, None if native else size, workers)
+        if native:
+            return load_image_folder(data_folder, None, workers, max_side=ragged_side_cap(size), dense_size=size)
+        return load_image_folder(data_folder, size, workers)
     raise ValueError(f"dataset not supported: {dataset}")

@@ -103,6 +103,17 @@ class PretrainEngine:
                 self._setup_syncbn_comm(opt, dev)
         if world > 1 and self.backend == "native":
             self._setup_gather_comm(opt, dev)
+        emu = int(os.environ.get("SDX_SYNCBN_EMU", "0") or 0)
+        if emu > 1 and world == 1 and self.backend == "native" and dev.type == "cuda":
+            # SyncBN over `emu` identical virtual ranks on this GPU (comm.EmulatedGroup):
+            # SDX_SYNCBN_EMU_KIND=fused (default, the xGMI fused exchange) | emu (reduce ->
+            # x·W -> finalize, the kernel sequence of the RCCL path minus the collective)
+            self.sync_group = comm.EmulatedGroup(emu)
+            m = _ext.require()
+            kind = os.environ.get("SDX_SYNCBN_EMU_KIND", "fused")
+            h = m.xgmi_emu_small_comm(emu) if kind == "fused" else m.emu_small_comm(emu)
+            comm.set_native_small_comm(self.sync_group, h)
+            logging.info(f"SyncBN emulated over {emu} virtual ranks ({kind})")
         model = model.to(dev)
         if dev.type == "cuda":
             model = model.to(memory_format=torch.channels_last)
@@ -146,27 +157,31 @@ class PretrainEngine:
     def _setup_syncbn_comm(self, opt, dev):
         """SyncBN statistics transport for the native backend.
 
-        ``--syncbn_comm xgmi``: one-shot IPC arena (every rank stores its payload into
-        every peer, one flag round trip). ``rccl`` (default): a dedicated RCCL
-        communicator. Either is registered as a native handle, so the C++ block
-        executor all-reduces each BN's sums itself on the compute stream. gloo (CPU
-        tests, shared-GPU tests) keeps the Python collective path."""
-        want = getattr(opt, "syncbn_comm", "rccl")
+        ``--syncbn_comm auto`` (default) / ``xgmi``: the one-shot IPC arena, whose FUSED
+        path reduces, exchanges and finalizes every BN's statistics in one launch
+        (parallel/xgmi.py); ``auto`` uses it whenever all ranks are peers on one node and
+        falls back to RCCL otherwise. ``rccl``: a dedicated RCCL communicator. Either is
+        registered as a native handle, so the C++ block executor exchanges each BN's sums
+        itself on the compute stream. gloo (CPU tests, shared-GPU tests) keeps the Python
+        collective path."""
+        want = getattr(opt, "syncbn_comm", "auto")
         if dev.type != "cuda":
             return
         timeout = float(getattr(opt, "comm_timeout", 600.0))
-        if want == "xgmi":
+        if want in ("xgmi", "auto"):
             # set-up is agreed step by step across ranks (parallel/xgmi.py): either every
             # rank gets the arena or every rank raises here and falls back to RCCL together
             try:
                 from ..parallel.xgmi import OneShotAllReduce
                 impl = OneShotAllReduce(timeout_s=timeout)
+                self._xgmi = impl
                 comm.set_small_allreduce(None, impl)
-                comm.set_native_small_comm(None, _ext.require().xgmi_small_comm(impl.id, comm.rank(), timeout))
-                logging.info("SyncBN statistics: one-shot xGMI all-reduce (native executor)")
+                comm.set_native_small_comm(None, impl.handle)
+                logging.info("SyncBN statistics: fused one-shot xGMI exchange (native executor)")
                 return
             except Exception as e:  # noqa: BLE001
-                logging.warning(f"one-shot xGMI all-reduce unavailable ({e}); using RCCL")
+                (logging.warning if want == "xgmi" else logging.info)(
+                    f"one-shot xGMI exchange unavailable ({e}); using RCCL")
         if comm.backend() == "nccl" and os.environ.get("SDX_NATIVE_SYNCBN", "1") != "0":
             # 0 on every rank together when the dedicated communicator cannot be set up
             handle = comm.create_rccl_small_comm(None, timeout)

@@ -47,7 +47,7 @@ def _omask(like, training):
 
 
 def _world(group) -> int:
-    return dist.get_world_size(group) if group is not None else 1
+    return comm.group_size(group)
 
 
 class _BN:

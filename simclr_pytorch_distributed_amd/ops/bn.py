@@ -19,6 +19,7 @@ import torch
 import torch.distributed as dist
 
 from . import _ext
+from ..parallel import comm
 
 
 def _allreduce(t: torch.Tensor, group):
@@ -28,7 +29,7 @@ def _allreduce(t: torch.Tensor, group):
 
 
 def _world(group) -> int:
-    return dist.get_world_size(group) if group is not None else 1
+    return comm.group_size(group)
 
 
 def _gscale(group) -> float:

@@ -28,6 +28,28 @@ def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+class EmulatedGroup:
+    """W identical virtual ranks on ONE GPU standing in for a SyncBN process group
+    (``SDX_SYNCBN_EMU=W``; tools/syncbn_latency.py, bench at world 1). Registered with an
+    emulated native communicator (comm_ops.cpp: EMU = reduce -> x·W -> finalize, or XEMU =
+    the fused xGMI exchange through W device-memory arenas), every BN of the native
+    executor runs its full cross-rank kernel sequence while the statistics stay exactly the
+    single-process ones — so the step time shows the SyncBN cost minus the xGMI link
+    latency, on the one-GPU box."""
+
+    def __init__(self, world: int):
+        self.world = int(world)
+
+
+def group_size(group) -> int:
+    """Ranks of a SyncBN group (None: 1; an :class:`EmulatedGroup`: its virtual ranks)."""
+    if group is None:
+        return 1
+    if isinstance(group, EmulatedGroup):
+        return group.world
+    return dist.get_world_size(group)
+
+
 def world_size() -> int:
     return dist.get_world_size() if is_dist() else 1
 

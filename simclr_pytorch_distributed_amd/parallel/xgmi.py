@@ -1,15 +1,25 @@
-"""One-shot small-message all-reduce over xGMI peer memory.
+"""One-shot small-message exchange over xGMI peer memory — the default
+SyncBN transport of the native executor when every rank is on one node.
 
-SyncBN issues one fp64 all-reduce of ``[2, C]`` statistics per BatchNorm layer in the
-forward pass and one of ``[2|3, C]`` sums in the backward pass (≈100 per ResNet-50 step,
-≤16 KiB each), all on the critical path. A ring collective pays 2(W−1) link hops per
-call; here every rank writes its payload once into every peer's IPC-mapped arena and
-publishes an epoch flag, so a call costs one xGMI write + one flag round trip
-(csrc/kernels/xgmi.hip). Arenas are exchanged once at start-up through the process group.
+SyncBN needs one fp64 sum of ``[2, C]`` statistics per BatchNorm layer in the forward pass
+and one of ``[2|3, C]`` sums in the backward pass (≈106 per ResNet-50 step, ≤24 KiB each;
+reference: main_supcon.py:222-224 → torch SyncBatchNorm), all on the critical path. A ring
+collective pays 2(W−1) link hops per call; here every rank writes its payload once into
+every peer's IPC-mapped arena and publishes an epoch flag, so a call costs one xGMI write
++ one flag round trip. Arenas are exchanged once at start-up through the process group.
+
+Two kernels use the arena:
+
+* the FUSED path (default): the BN statistics' column reduction itself (csrc/kernels/bn.hip
+  ``col_reduce`` with an ``XgmiCol``) stores each 64-channel group's sums into the peers'
+  arenas, waits for theirs and runs the finalize / backward-coefficient epilogue on the
+  global sums — reduce + all-reduce + finalize in ONE launch per BN;
+* ``all_reduce``: the stand-alone one-shot kernel (csrc/kernels/xgmi.hip) for any small fp64
+  tensor (``SDX_SYNCBN_FUSED=0`` routes the executor through it).
 
 Requires all ranks on ONE node (``LOCAL_WORLD_SIZE == WORLD_SIZE``) and ≤ 8 of them; the
-engine falls back to the RCCL all-reduce otherwise, or if the start-up self-check fails.
-Enabled with ``--syncbn_comm xgmi``.
+engine falls back to a dedicated RCCL communicator otherwise, or if a start-up self-check
+(stand-alone and fused exchange against known sums) fails on any rank.
 """
 from __future__ import annotations
 
@@ -28,7 +38,7 @@ class OneShotAllReduce:
     rank that fails to allocate or map raises on EVERY rank (after each rank destroyed
     its own arena), never only on itself while its peers wait in a collective."""
 
-    def __init__(self, group=None, cap: int = 8192, timeout_s: float = 600.0):
+    def __init__(self, group=None, cap: int = 12288, timeout_s: float = 600.0):
         from . import comm
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("process group not initialised")
@@ -38,6 +48,7 @@ class OneShotAllReduce:
         self.m = _ext.require()
         self.cap = cap
         self.id = None
+        self.handle = 0          # native small-communicator wrapping the arena (comm_ops.cpp)
         st = {}
 
         def check_topology():
@@ -59,7 +70,11 @@ class OneShotAllReduce:
         def open_peers():
             self.m.xgmi_open(self.id, st["h"])
 
-        ok, err = comm.negotiate([check_topology, create, exchange, open_peers, self._self_check], self.close, group)
+        def wrap():
+            self.handle = self.m.xgmi_small_comm(self.id, self.rank, float(timeout_s))
+
+        ok, err = comm.negotiate([check_topology, create, exchange, open_peers, self._self_check, wrap,
+                                  self._fused_check], self.close, group)
         if not ok:
             raise RuntimeError(f"one-shot xGMI all-reduce unavailable ({err if err is not None else 'on a peer rank'})")
 
@@ -73,6 +88,20 @@ class OneShotAllReduce:
         if not (err == 0 and torch.equal(out, exp)):
             raise RuntimeError(f"one-shot xGMI all-reduce self-check failed (err={err})")
 
+    def _fused_check(self):
+        """The fused SyncBN exchange (column reduction + exchange in one launch) on slabs
+        with rank-dependent values and the BN shapes' extremes: C = 64 (one group) and
+        C = 2048 with 3 sums (32 groups), rows 1 and 300."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        for rows, ns, C in ((1, 2, 64), (300, 3, 2048), (37, 2, 200)):
+            base = torch.arange(rows * ns * C, dtype=torch.float64, device=dev).remainder(97).view(rows, ns, C)
+            slab = (base + self.rank).float()
+            got = self.m.syncbn_exchange_sums(self.handle, slab.contiguous())
+            exp = base.sum(0) * self.world + rows * sum(range(self.world))
+            torch.cuda.synchronize()
+            if self.m.xgmi_error(self.id) != 0 or not torch.allclose(got, exp, rtol=0, atol=1e-6):
+                raise RuntimeError(f"fused xGMI SyncBN exchange self-check failed (rows {rows}, C {C})")
+
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         """Sum over ranks of a small fp64 tensor (returns a new tensor)."""
         if x.numel() > self.cap:
@@ -84,6 +113,11 @@ class OneShotAllReduce:
         return x
 
     def close(self):
+        # the wrapping communicator first: the watchdog must stop sweeping the arena before
+        # it is freed
+        if getattr(self, "handle", 0):
+            self.m.small_comm_destroy(self.handle)
+            self.handle = 0
         if getattr(self, "id", None) is not None:
             self.m.xgmi_destroy(self.id)
             self.id = None

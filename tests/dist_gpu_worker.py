@@ -19,19 +19,20 @@ def main():
     from simclr_pytorch_distributed_amd.models.executor import to_nhwc_input
     from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
     from simclr_pytorch_distributed_amd.parallel import comm
-    B = 16                                    # images per rank
-    G = 32                                    # global images
-    argv = ["--model", "resnet18", "--backend", "native", "--dist_backend", "gloo", "--synthetic",
+    name = os.environ.get("SDX_TEST_MODEL", "resnet18")
+    G = 32                                    # global images (16 per rank at W=2: 32 views, so
+    #                                           ResNet-50 layer 1 folds its BN3 on every rank)
+    argv = ["--model", name, "--backend", "native", "--dist_backend", "gloo", "--synthetic",
             "--synthetic_size", "64", "--learning_rate", "0.05", "--grad_semantics", "exact",
             "--work_dir", out_dir, "--batch_size", str(G), "--ngpu", str(world)]
     if world > 1:
         argv.append("--syncBN")
-        if os.environ.get("SDX_TEST_SYNCBN_COMM"):
-            argv += ["--syncbn_comm", os.environ["SDX_TEST_SYNCBN_COMM"]]
+        # '' = rccl, which over the gloo process group means the Python collective path
+        argv += ["--syncbn_comm", os.environ.get("SDX_TEST_SYNCBN_COMM") or "rccl"]
     opt = parse_pretrain(argv, make_dirs=False)
     eng = PretrainEngine(opt, device=torch.device("cuda:0"))
     torch.manual_seed(123)
-    init = SupConResNet("resnet18").state_dict()
+    init = SupConResNet(name).state_dict()
     eng.model.load_state_dict(init)
     eng.model.train()
     g = torch.Generator().manual_seed(7)
@@ -51,7 +52,7 @@ def main():
     bn = eng.model.encoder.layer1[0].bn1
     torch.save({"flat": eng.flat.flat.detach().cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
                 "native_h": comm.native_small_comm(None), "loss": float(loss.detach()), "grad": grad.cpu(), "names": list(eng.flat.names),
-                "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"w{world}_r{rank}.pt"))
+                "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"{name}_w{world}_r{rank}.pt"))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

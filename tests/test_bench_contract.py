@@ -39,6 +39,22 @@ def test_bench_two_ranks_json_contract(tmp_path):
     assert abs(d["value"] - 8 * 1e3 / d["ms_per_step"]) / d["value"] < 0.01
 
 
+def test_bench_self_launches_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no external launcher starts its own 2 ranks
+    (torch.distributed.run as a child process) and relays rank 0's JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "SDX_BENCH_CHILD")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--backend", "torch", "--model", "resnet18", "--per_gpu_batch", "4"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2+syncbn"
+    assert d["config"]["global_batch"] == 8
+
+
 def test_bench_global_batch_is_strong_scaling(tmp_path):
     """--global_batch fixes the total batch (README headline: BS 256 over 2 GPUs)."""
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")

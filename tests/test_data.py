@@ -34,6 +34,20 @@ def test_image_folder_native_and_resized(tmp_path):
     assert not dense.ragged and dense.images.shape == (len(shapes), 16, 16, 3)
 
 
+def test_image_folder_side_cap_and_budget(tmp_path):
+    """The ragged store caps the shorter side at ragged_side_cap(size) (aspect kept) and
+    falls back to the dense resized store when it would exceed the byte budget."""
+    from simclr_pytorch_distributed_amd.data.datasets import load_image_folder, ragged_side_cap
+    assert ragged_side_cap(32) == 83 and ragged_side_cap(224) == 579
+    _folder(tmp_path, [(120, 60), (40, 200), (30, 30)])
+    ds = load_image_folder(str(tmp_path), None, 2, max_side=50)
+    hw = sorted(tuple(int(v) for v in s) for s in ds.sizes)
+    assert hw == sorted([(100, 50), (40, 200), (30, 30)])
+    assert ds.images.size == sum(h * w * 3 for h, w in hw)
+    small = load_image_folder(str(tmp_path), None, 2, max_side=50, budget_bytes=1000, dense_size=16)
+    assert not small.ragged and small.images.shape == (3, 16, 16, 3)
+
+
 def test_ragged_reference_augment_matches_dense():
     """Same-size images: the ragged CPU path reproduces the dense one exactly."""
     from simclr_pytorch_distributed_amd.data.augment import AugConfig, augment_reference

@@ -14,12 +14,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _launch(world, out, syncbn_comm=""):
+def _launch(world, out, syncbn_comm="", model="resnet18"):
     # file-store rendezvous: no probed TCP port that another job on the box can take first
-    rdv = os.path.join(str(out), f"rdv_{world}_{syncbn_comm or 'pg'}")
+    rdv = os.path.join(str(out), f"rdv_{model}_{world}_{syncbn_comm or 'pg'}")
     procs = []
     for r in range(world):
-        env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world),
+        env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, SDX_TEST_MODEL=model, RANK=str(r), LOCAL_RANK="0",
+                   WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD="file://" + rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -33,15 +34,21 @@ def _launch(world, out, syncbn_comm=""):
         assert p.returncode == 0, err[-3000:]
 
 
-@pytest.mark.parametrize("syncbn_comm", ["", "xgmi"])
-def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, syncbn_comm):
+@pytest.mark.parametrize("model,syncbn_comm", [("resnet18", ""), ("resnet18", "xgmi"), ("resnet50", ""),
+                                               ("resnet50", "xgmi")])
+def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, model, syncbn_comm):
     """'': SyncBN statistics over gloo (Python block path); 'xgmi': the one-shot IPC arena
-    registered as a native handle, so the C++ block executor issues every BN all-reduce."""
-    _launch(1, tmp_path)
-    _launch(2, tmp_path, syncbn_comm)
-    ref = torch.load(tmp_path / "w1_r0.pt", weights_only=True)
-    a = torch.load(tmp_path / "w2_r0.pt", weights_only=True)
-    b = torch.load(tmp_path / "w2_r1.pt", weights_only=True)
+    registered as a native handle, so the C++ block executor exchanges every BN's statistics
+    through the FUSED path (reduce + exchange + epilogue in one launch, two real processes
+    on this GPU). ResNet-50 (the reference's flagship, main_supcon.py:222-234) exercises
+    the bottleneck executor with the layer-1 BN3 / shortcut folds under SyncBN: every
+    parameter gradient of the W=2 step must match the W=1 step on the concatenated batch
+    (worst relative error printed, bounded at 2e-2)."""
+    _launch(1, tmp_path, "", model)
+    _launch(2, tmp_path, syncbn_comm, model)
+    ref = torch.load(tmp_path / f"{model}_w1_r0.pt", weights_only=True)
+    a = torch.load(tmp_path / f"{model}_w2_r0.pt", weights_only=True)
+    b = torch.load(tmp_path / f"{model}_w2_r1.pt", weights_only=True)
     if syncbn_comm == "xgmi":
         assert a["native_h"] > 0 and b["native_h"] > 0, "xGMI small communicator was not registered"
     bad = [n for n, o, k in zip(a["names"], a["offsets"], a["numels"])
@@ -49,7 +56,6 @@ def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, syncbn_comm):
     assert not bad, f"all-reduced gradients differ across ranks for {len(bad)} params: {bad[:12]}"
     assert torch.equal(a["flat"], b["flat"])                  # replicas stay identical
     assert torch.equal(a["rm"], b["rm"])                      # SyncBN running stats identical
-    init = torch.load(tmp_path / "w1_r0.pt", weights_only=True)
     d_ref = ref["flat"] - a["flat"]
     rel = d_ref.norm() / (ref["flat"].norm() + 1e-12)
     assert rel < 2e-3, float(rel)
@@ -62,6 +68,9 @@ def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, syncbn_comm):
         g1, g2 = ref["grad"][o:o + k].double(), a["grad"][o:o + k].double()
         worst.append((float((g2 - g1).norm() / (g1.norm() + 1e-12)), n))
     worst.sort(reverse=True)
-    assert worst[0][0] < 5e-2, worst[:8]
+    print(f"{model} W=2 ({syncbn_comm or 'gloo'}) vs W=1: {len(worst)} parameters, worst rel "
+          + ", ".join(f"{n} {r:.3g}" for r, n in worst[:4]))
+    assert len(worst) == (163 if model == "resnet50" else 64)
+    assert worst[0][0] < 2e-2, worst[:8]
     # global loss = sum of the ranks' row-owned losses
     assert abs(a["loss"] + b["loss"] - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3
