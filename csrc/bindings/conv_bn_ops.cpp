@@ -145,7 +145,7 @@ StatFuse make_fuse(FuseReq& r, const torch::Tensor& like, int64_t M, int64_t Nco
 
 std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad,
                                          bool want_stats, int64_t cfg, OptT in_scale, OptT in_shift,
-                                         FuseReq* fr) {
+                                         FuseReq* fr, const GemmEpi* epi = nullptr) {
   check_bf16_nhwc(x, "x");
   check_bf16_nhwc(w, "w");
   TORCH_CHECK(w.size(3) == x.size(3), "weight Cin != input C");
@@ -180,9 +180,19 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
     sf = make_fuse(*fr, x, M, g.K, (int)cfg, 2, lvl2);
   }
   check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream(), isc, ish,
-                            nullptr, fr != nullptr ? &sf : nullptr),
+                            epi, fr != nullptr ? &sf : nullptr),
             "conv_fwd");
   return {y, slab};
+}
+
+// conv with a per-output-channel fp32 bias (+ ReLU) applied to the fp32 accumulators before
+// the bf16 rounding, no statistics: an eval-mode conv + BatchNorm (+ ReLU) with the BN
+// folded into the weights and the bias (linear-probe encoder, ops/linear_probe.py)
+torch::Tensor conv_fwd_bias(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, torch::Tensor bias,
+                            bool relu) {
+  check_vec(bias, w.size(0), "bias");
+  const GemmEpi epi{bias.data_ptr<float>(), relu ? 1 : 0, 0, 0};
+  return conv_fwd_impl(x, w, stride, pad, false, -1, c10::nullopt, c10::nullopt, nullptr, &epi)[0];
 }
 
 std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
@@ -1468,6 +1478,10 @@ torch::Tensor syncbn_exchange_sums(int64_t comm, torch::Tensor slab) {
 }  // namespace
 
 void register_conv_bn(pybind11::module& m) {
+  m.def("conv_fwd_bias", &conv_fwd_bias,
+        "implicit-GEMM conv forward with a per-channel fp32 bias (+ReLU) epilogue (eval-mode folded BN)",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("bias"),
+        pybind11::arg("relu"));
   m.def("syncbn_exchange_sums", &syncbn_exchange_sums,
         "column reduction + cross-rank exchange of a BN statistics slab in one launch (fused xGMI communicators)");
   m.def("stat_fuse_set", &stat_fuse_set,

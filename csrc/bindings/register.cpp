@@ -11,6 +11,7 @@ void register_wprep(pybind11::module& m);
 void register_xgmi(pybind11::module& m);
 void register_comm(pybind11::module& m);
 void register_head(pybind11::module& m);
+void register_probe(pybind11::module& m);
 
 void register_ops(pybind11::module& m) {
   register_supcon(m);
@@ -22,5 +23,6 @@ void register_ops(pybind11::module& m) {
   register_xgmi(m);
   register_comm(m);
   register_head(m);
+  register_probe(m);
 }
 }  // namespace sdx_bind

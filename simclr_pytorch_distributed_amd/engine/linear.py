@@ -7,7 +7,11 @@ validation top-1 (and the top-5 of that epoch), as in main_linear.py:284-288.
 Fixes vs reference: checkpoint weights are always loaded (prefix-tolerant),
 independent of GPU count. Augmentation runs on the GPU (RandomResizedCrop + flip +
 normalize for training, normalize for validation) from the HBM-resident dataset.
-Encoder features of the validation set are computed once per epoch in large batches.
+
+Native backend (ops/linear_probe.py): the frozen encoder runs with every
+eval-mode BatchNorm folded into its conv (one implicit-GEMM launch per conv + BN + ReLU, no
+BN kernels), and the classifier's logits, cross-entropy, top-1/5 hits, gradient and SGD
+update are two fused launches per batch; the meters stay on the device.
 """
 from __future__ import annotations
 
@@ -59,6 +63,13 @@ class LinearEngine:
         self.model = model
         self.runner = ModelRunner(model, self.backend, opt.precision)
         self.classifier = LinearClassifier(opt.model, opt.n_cls).to(dev)
+        self.folded = None
+        self.native_ce = None
+        if self.backend == "native":
+            from ..ops import linear_probe
+            self.folded = linear_probe.FoldedEncoder(model.encoder)
+            if linear_probe.supported(self.classifier):
+                self.native_ce = linear_probe.NativeLinearCE(self.classifier, opt.momentum, opt.weight_decay)
         self.criterion = torch.nn.CrossEntropyLoss()
         self.optimizer = torch.optim.SGD(self.classifier.parameters(), lr=opt.learning_rate, momentum=opt.momentum,
                                          weight_decay=opt.weight_decay)
@@ -81,7 +92,27 @@ class LinearEngine:
         if self.backend == "torch":
             x = nhwc8_to_nchw(x)
         with torch.no_grad():
+            if self.folded is not None:
+                return self.folded(x)
             return self.runner.encode(x, training=False).float()
+
+    def _classify(self, feats, labels, train: bool):
+        """(logits, loss, acc1, acc5) of a batch — device tensors; train: + the SGD step."""
+        bsz = labels.shape[0]
+        if self.native_ce is not None:
+            if train:
+                out, st = self.native_ce.train_batch(feats, labels, self.optimizer.param_groups[0]["lr"])
+            else:
+                out, st = self.native_ce.eval_batch(feats, labels)
+            return out, st[0] / bsz, st[1] * (100.0 / bsz), st[2] * (100.0 / bsz)
+        output = self.classifier(feats.detach())
+        loss = self.criterion(output, labels)
+        acc1, acc5 = accuracy(output, labels, topk=(1, 5))
+        if train:
+            self.optimizer.zero_grad()
+            loss.backward()
+            self.optimizer.step()
+        return output, loss.detach(), acc1[0], acc5[0]
 
     def train_epoch(self, epoch):
         opt = self.opt
@@ -108,13 +139,8 @@ class LinearEngine:
             with ph("encoder"):
                 feats = self._features(x)
             with ph("classifier"):
-                output = self.classifier(feats.detach())
-                loss = self.criterion(output, labels)
-                acc1, acc5 = accuracy(output, labels, topk=(1, 5))
-                self.optimizer.zero_grad()
-                loss.backward()
-                self.optimizer.step()
-                win += torch.stack([loss.detach().double() * bsz, acc1[0].double() * bsz, acc5[0].double() * bsz,
+                output, loss, acc1, acc5 = self._classify(feats, labels, True)
+                win += torch.stack([loss.double() * bsz, acc1.double() * bsz, acc5.double() * bsz,
                                     torch.tensor(float(bsz), dtype=torch.float64, device=self.device)])
             bt.update(time.time() - end)
             if (idx_i + 1) % opt.print_freq == 0 or idx_i + 1 == iters:
@@ -123,7 +149,7 @@ class LinearEngine:
                 losses.update(sl / nb, nb)
                 losses.val = loss.item()
                 top1.update(s1 / nb, nb)
-                top1.val = acc1[0].item()
+                top1.val = acc1.item()
                 top5.update(s5 / nb, nb)
                 logging.info("Train: [{0}][{1}/{2}]\tBT {bt.val:.3f} ({bt.avg:.3f})\t"
                              "DT {dt.val:.3f} ({dt.avg:.3f})\tloss {loss.val:.3f} ({loss.avg:.3f})\t"
@@ -146,13 +172,11 @@ class LinearEngine:
             idx = torch.arange(s, min(s + vb, n), device=self.device)
             x = augment(self.va_x, idx, self.aug_val, 0)
             labels = self.va_y[idx]
-            output = self.classifier(self._features(x))
-            loss = self.criterion(output, labels)
-            acc1, acc5 = accuracy(output, labels, topk=(1, 5))
+            output, loss, acc1, acc5 = self._classify(self._features(x), labels, False)
             bsz = labels.shape[0]
             losses.update(loss.item(), bsz)
-            top1.update(acc1[0].item(), bsz)
-            top5.update(acc5[0].item(), bsz)
+            top1.update(acc1.item(), bsz)
+            top5.update(acc5.item(), bsz)
             if i % opt.print_freq == 0:
                 logging.info("Test: [{0}/{1}]\tLoss {loss.val:.4f} ({loss.avg:.4f})\t"
                              "Acc@1 {top1.val:.3f} ({top1.avg:.3f})".format(
