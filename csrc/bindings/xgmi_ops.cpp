@@ -3,7 +3,9 @@
 // the single-GPU W-rank emulation used by the tests.
 #include "ops_decl.h"
 #include "launchers.h"
+#include "conv_internal.h"
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -23,7 +25,14 @@ struct Arena {
   unsigned epoch = 0;
   int* err = nullptr;              // host-pinned, GPU-written error word (sender index + 1)
   long long timeout_ticks = 0;     // flag-poll deadline in 100 MHz wall-clock ticks
+  double ticks_per_s = 1e8;        // wall-clock rate
 };
+
+// a per-call deadline (start-up self-checks: seconds, not --comm_timeout) capped by the arena's
+long long call_ticks(const Arena& a, double timeout_s) {
+  if (!(timeout_s > 0)) return a.timeout_ticks;
+  return std::min(a.timeout_ticks, std::max(1LL, (long long)(timeout_s * a.ticks_per_s)));
+}
 
 std::mutex g_mu;
 std::vector<std::unique_ptr<Arena>> g_arenas;
@@ -68,7 +77,8 @@ int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, double timeout_s) 
   *reinterpret_cast<volatile int*>(a->err) = 0;
   int rate_khz = 0;
   check_hip(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, a->device), "wall clock rate");
-  a->timeout_ticks = (long long)(timeout_s * 1000.0 * (rate_khz > 0 ? rate_khz : 100000));
+  a->ticks_per_s = 1000.0 * (rate_khz > 0 ? rate_khz : 100000);
+  a->timeout_ticks = (long long)(timeout_s * a->ticks_per_s);
   std::lock_guard<std::mutex> lk(g_mu);
   g_arenas.push_back(std::move(a));
   return (int64_t)g_arenas.size() - 1;
@@ -100,7 +110,7 @@ void xgmi_open(int64_t id, torch::Tensor handles) {
   }
 }
 
-torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x) {
+torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x, double timeout_s) {
   Arena& a = get(id);
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.is_contiguous(), "x: contiguous fp64 GPU tensor");
   TORCH_CHECK((size_t)x.numel() <= a.cap, "message larger than the arena slot");
@@ -108,7 +118,7 @@ torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x) {
   auto out = torch::empty_like(x);
   a.epoch += 1;
   check_hip(launch_xgmi_allreduce(x.data_ptr<double>(), out.data_ptr<double>(), (int)x.numel(), a.peers, a.rank,
-                                  a.world, a.epoch, a.err, a.timeout_ticks, cur_stream()),
+                                  a.world, a.epoch, a.err, call_ticks(a, timeout_s), cur_stream()),
             "xgmi_allreduce");
   return out;
 }
@@ -152,7 +162,8 @@ int64_t xgmi_emu_create(int64_t world, int64_t cap, double timeout_s) {
   *reinterpret_cast<volatile int*>(a->err) = 0;
   int rate_khz = 0;
   check_hip(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, a->device), "wall clock rate");
-  a->timeout_ticks = (long long)(timeout_s * 1000.0 * (rate_khz > 0 ? rate_khz : 100000));
+  a->ticks_per_s = 1000.0 * (rate_khz > 0 ? rate_khz : 100000);
+  a->timeout_ticks = (long long)(timeout_s * a->ticks_per_s);
   std::lock_guard<std::mutex> lk(g_mu);
   g_arenas.push_back(std::move(a));
   return (int64_t)g_arenas.size() - 1;
@@ -205,10 +216,33 @@ XgmiCol xgmi_col_args(int64_t id) {
   return x;
 }
 bool xgmi_emulated(int64_t id) { return get(id).emulated; }
+
+// The fused SyncBN exchange (bn.hip col_reduce + XgmiCol) of a statistics slab directly on
+// an arena, with a per-call deadline: the start-up self-check runs it BEFORE the arena is
+// wrapped as a small communicator, so a peer that never answers makes the check fail (and
+// every rank fall back to RCCL) instead of tripping the communicator watchdog.
+// slab [rows][nsets][C] fp32 -> global sums [nsets][C] (fp64).
+torch::Tensor xgmi_exchange_sums(int64_t id, torch::Tensor slab, double timeout_s) {
+  TORCH_CHECK(slab.is_cuda() && slab.scalar_type() == at::kFloat && slab.is_contiguous() && slab.dim() == 3,
+              "slab: contiguous fp32 [rows][nsets][C]");
+  const int64_t rows = slab.size(0), nsets = slab.size(1), C = slab.size(2);
+  TORCH_CHECK(rows >= 1 && nsets >= 1 && nsets <= 3 && C >= 1 && C <= 4096, "slab shape");
+  XgmiCol x = xgmi_col_args(id);
+  x.timeout_ticks = call_ticks(get(id), timeout_s);
+  c10::DeviceGuard dg(slab.device());
+  const int z = x.mode == 2 ? x.world : 1;
+  auto sums = torch::empty({nsets, C}, slab.options().dtype(at::kDouble));
+  auto scratch = reduce_scratch(slab, rows, nsets, C, z);
+  check_hip(launch_col_reduce(slab.data_ptr<float>(), (int)rows, (int)nsets, (int)C, scratch.data_ptr<double>(),
+                              reduce_counters(slab.device(), z), sums.data_ptr<double>(), 0, nullptr, nullptr,
+                              cur_stream(), &x),
+            "xgmi_exchange_sums");
+  return sums;
+}
 int64_t xgmi_emu_create_ext(int64_t world, int64_t cap, double timeout_s) { return xgmi_emu_create(world, cap, timeout_s); }
 
 // for comm_ops.cpp (small-communicator wrapper of an arena)
-torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x) { return xgmi_allreduce(id, x); }
+torch::Tensor xgmi_allreduce_ext(int64_t id, torch::Tensor x) { return xgmi_allreduce(id, x, -1.0); }
 int64_t xgmi_world(int64_t id) { return get(id).world; }
 int64_t xgmi_error_ext(int64_t id) { return xgmi_error(id); }
 // watchdog sweep: never throws; 0 once the arena is gone (the read happens under the
@@ -228,7 +262,11 @@ void register_xgmi(pybind11::module& m) {
         pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("cap"), pybind11::arg("timeout_s") = 600.0);
   m.def("xgmi_handle", &xgmi_handle, "64-byte IPC handle of this rank's arena");
   m.def("xgmi_open", &xgmi_open, "map every peer's arena from their IPC handles [W, 64]");
-  m.def("xgmi_allreduce", &xgmi_allreduce, "one-shot fp64 all-reduce (sum) of a small tensor");
+  m.def("xgmi_allreduce", &xgmi_allreduce, "one-shot fp64 all-reduce (sum) of a small tensor",
+        pybind11::arg("id"), pybind11::arg("x"), pybind11::arg("timeout_s") = -1.0);
+  m.def("xgmi_exchange_sums", &xgmi_exchange_sums,
+        "fused SyncBN exchange of a [rows][nsets][C] statistics slab on an arena (per-call deadline)",
+        pybind11::arg("id"), pybind11::arg("slab"), pybind11::arg("timeout_s") = -1.0);
   m.def("xgmi_error", &xgmi_error, "nonzero: a peer's flag never arrived (1 + sender)");
   m.def("xgmi_destroy", &xgmi_destroy);
   m.def("xgmi_debug", &xgmi_debug);

@@ -38,6 +38,8 @@ class OneShotAllReduce:
     rank that fails to allocate or map raises on EVERY rank (after each rank destroyed
     its own arena), never only on itself while its peers wait in a collective."""
 
+    CHECK_TIMEOUT_S = 30.0   # deadline of each start-up self-check kernel
+
     def __init__(self, group=None, cap: int = 12288, timeout_s: float = 600.0):
         from . import comm
         if not (dist.is_available() and dist.is_initialized()):
@@ -73,15 +75,18 @@ class OneShotAllReduce:
         def wrap():
             self.handle = self.m.xgmi_small_comm(self.id, self.rank, float(timeout_s))
 
-        ok, err = comm.negotiate([check_topology, create, exchange, open_peers, self._self_check, wrap,
-                                  self._fused_check], self.close, group)
+        # the checks run on the bare arena with a short deadline: a peer that never answers
+        # fails the check on every rank (-> RCCL fallback); only a checked arena is wrapped
+        # (and so watched by the communicator watchdog)
+        ok, err = comm.negotiate([check_topology, create, exchange, open_peers, self._self_check, self._fused_check,
+                                  wrap], self.close, group)
         if not ok:
             raise RuntimeError(f"one-shot xGMI all-reduce unavailable ({err if err is not None else 'on a peer rank'})")
 
     def _self_check(self):
         dev = torch.device("cuda", torch.cuda.current_device())
         x = torch.arange(16, dtype=torch.float64, device=dev) + 100.0 * self.rank
-        out = self.all_reduce(x)
+        out = self.m.xgmi_allreduce(self.id, x, self.CHECK_TIMEOUT_S)
         torch.cuda.synchronize()
         err = self.m.xgmi_error(self.id)
         exp = torch.arange(16, dtype=torch.float64, device=dev) * self.world + 100.0 * sum(range(self.world))
@@ -96,7 +101,7 @@ class OneShotAllReduce:
         for rows, ns, C in ((1, 2, 64), (300, 3, 2048), (37, 2, 200)):
             base = torch.arange(rows * ns * C, dtype=torch.float64, device=dev).remainder(97).view(rows, ns, C)
             slab = (base + self.rank).float()
-            got = self.m.syncbn_exchange_sums(self.handle, slab.contiguous())
+            got = self.m.xgmi_exchange_sums(self.id, slab.contiguous(), self.CHECK_TIMEOUT_S)
             exp = base.sum(0) * self.world + rows * sum(range(self.world))
             torch.cuda.synchronize()
             if self.m.xgmi_error(self.id) != 0 or not torch.allclose(got, exp, rtol=0, atol=1e-6):
