@@ -60,13 +60,34 @@ __device__ __forceinline__ void split_hi_lo(float x, uint16_t& hi, uint16_t& lo)
   lo = f2bf(x - bf2f(hi));
 }
 
+// LDS image of the 32 staged other rows (bf16 hi and lo images). D >= 128: unpadded
+// 2D-byte rows with the 16-B chunk index XOR-swizzled by sw(r) = ((r & 7) << 1) | (r >> 3 & 1):
+//   * tile-product ds_read_b128 (16 lanes = 16 consecutive rows, one chunk): 16 distinct
+//     slots of the 256-B bank row;
+//   * backward ds_read_b64_tr_b16 (32 lanes = 8 consecutive rows x 2 adjacent chunks):
+//     sw maps rows 0..7 to distinct even (8..15 to odd) values, so 16 distinct slots;
+//   * staging writes (16 lanes = the 16 chunks of one row): a bijection per row.
+// (The earlier +16-B row padding left 2-way conflicts on the transposed reads and 4-way on
+// the staging writes: ~50 % LDS bank conflicts at N = 8192, profiles/pmc_conv_supcon_r1_v2.txt.)
+// D = 64 keeps the padded rows.
+template <int D>
+__device__ __forceinline__ int sc_off(int row, int byte) {
+  if constexpr (D >= 128) {
+    const int sw = ((row & 7) << 1) | ((row >> 3) & 1);
+    return row * (D * 2) + ((((byte >> 4) ^ sw)) << 4) + (byte & 15);
+  } else {
+    return row * (D * 2 + 16) + byte;
+  }
+}
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
   constexpr int KS = D / 32;                 // MFMA k-steps over the feature dim
-  constexpr int RS = D * 2 + 16;             // padded LDS row stride (bytes) of a bf16 row
+  constexpr int RS = D >= 128 ? D * 2 : D * 2 + 16;   // LDS row stride (bytes) of a bf16 row
   constexpr int TILE_BYTES = OTHER_TILE * RS;
   constexpr int STAGE_BYTES = 2 * TILE_BYTES;             // hi + lo
-  constexpr int OUT_BYTES = (MODE == MODE_FWD) ? 0 : OWN_PER_WG * D * 4;
+  constexpr int OSTR = D + 4;                // fp32 transpose rows padded by 16 B (bank spread)
+  constexpr int OUT_BYTES = (MODE == MODE_FWD) ? 0 : OWN_PER_WG * OSTR * 4;
   constexpr int LDS_BYTES = STAGE_BYTES > OUT_BYTES ? STAGE_BYTES : OUT_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   unsigned char* lds_hi = smem;
@@ -124,19 +145,19 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
   if (o_end > p.n_other) o_end = p.n_other;
 
   for (int ob = o_begin; ob < o_end; ob += OTHER_TILE) {
-    // ---- stage 32 other rows into LDS as bf16 hi/lo ----
+    // ---- stage 32 other rows into LDS as bf16 hi/lo: thread = one 8-float chunk, the 16..32
+    // lanes of a row adjacent (coalesced 32-B global reads, conflict-free LDS writes) ----
     {
-      constexpr int TPR = 256 / OTHER_TILE;          // threads per row (8)
-      constexpr int FPT = D / TPR;                   // floats per thread (16 @ D=128)
-      const int r = tid / TPR;
-      const int c0 = (tid % TPR) * FPT;
-      const int orow = ob + r;
-      const bool ok = orow < o_end;
+      constexpr int CPR = D / 8;                     // 16-B bf16 chunks per row
+      constexpr int RPP = 256 / CPR;                 // rows per pass
 #pragma unroll
-      for (int f = 0; f < FPT; f += 8) {
+      for (int pass = 0; pass < OTHER_TILE / RPP; ++pass) {
+        const int r = pass * RPP + tid / CPR;
+        const int k = tid % CPR;
+        const int orow = ob + r;
         float xs[8];
-        if (ok) {
-          const float4* src = reinterpret_cast<const float4*>(p.other + (size_t)orow * D + c0 + f);
+        if (orow < o_end) {
+          const float4* src = reinterpret_cast<const float4*>(p.other + (size_t)orow * D + 8 * k);
           const float4 v0 = src[0], v1 = src[1];
           xs[0] = v0.x; xs[1] = v0.y; xs[2] = v0.z; xs[3] = v0.w;
           xs[4] = v1.x; xs[5] = v1.y; xs[6] = v1.z; xs[7] = v1.w;
@@ -152,8 +173,9 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
         vh.z = hh[4] | (hh[5] << 16); vh.w = hh[6] | (hh[7] << 16);
         vl.x = ll[0] | (ll[1] << 16); vl.y = ll[2] | (ll[3] << 16);
         vl.z = ll[4] | (ll[5] << 16); vl.w = ll[6] | (ll[7] << 16);
-        *reinterpret_cast<uint4*>(lds_hi + r * RS + (c0 + f) * 2) = vh;
-        *reinterpret_cast<uint4*>(lds_lo + r * RS + (c0 + f) * 2) = vl;
+        const int o = sc_off<D>(r, 16 * k);
+        *reinterpret_cast<uint4*>(lds_hi + o) = vh;
+        *reinterpret_cast<uint4*>(lds_lo + o) = vl;
       }
     }
     __syncthreads();
@@ -165,7 +187,7 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
       acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int off = (16 * t + c) * RS + (32 * s + 8 * h) * 2;
+        const int off = sc_off<D>(16 * t + c, (32 * s + 8 * h) * 2);
         const bf16x8 a_hi = *reinterpret_cast<const bf16x8*>(lds_hi + off);
         const bf16x8 a_lo = *reinterpret_cast<const bf16x8*>(lds_lo + off);
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hi, ob_hi[s], acc[t], 0, 0, 0);
@@ -236,7 +258,7 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
         bf16x8 a2_hi, a2_lo;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
-          const int off = (16 * tt + 4 * h + qq) * RS + (16 * q + 4 * pp) * 2;
+          const int off = sc_off<D>(16 * tt + 4 * h + qq, (16 * q + 4 * pp) * 2);
           const bf16x4 th = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds_hi + off));
           const bf16x4 tl = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds_lo + off));
 #pragma unroll
@@ -282,7 +304,7 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
 #pragma unroll
     for (int q = 0; q < D / 16; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out_lds[(wv * 16 + c) * D + 16 * q + 4 * h + r] = acc2[q][r];
+      for (int r = 0; r < 4; ++r) out_lds[(wv * 16 + c) * OSTR + 16 * q + 4 * h + r] = acc2[q][r];
     __syncthreads();
     float* slice = p.out + (size_t)blockIdx.y * p.n_own * D;
     for (int rr = 0; rr < 16; ++rr) {
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(256) void supcon_tile_kernel(SupconParams p) {
 #pragma unroll
       for (int d = 4 * lane; d < D; d += 256)
         *reinterpret_cast<float4*>(slice + (size_t)orow * D + d) =
-            *reinterpret_cast<const float4*>(out_lds + (wv * 16 + rr) * D + d);
+            *reinterpret_cast<const float4*>(out_lds + (wv * 16 + rr) * OSTR + d);
     }
   }
 }

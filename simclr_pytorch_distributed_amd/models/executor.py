@@ -6,10 +6,14 @@ this executor walks them and issues the fused native ops instead of ``nn.Conv2d`
 
 * activations NHWC bf16, produced and consumed by the implicit-GEMM MFMA conv kernels;
 * every conv (training) emits its BN statistics from the epilogue; every BN+ReLU (and
-  BN+shortcut-BN+add+ReLU) is one fused elementwise pass; SyncBN adds one fp64
-  all-reduce per BN;
-* global average pooling and the projection head run as stock torch ops on the
-  [views, 2048] feature matrix (tiny compared to the trunk).
+  BN+shortcut-BN+add+ReLU) is one fused elementwise pass; each residual block's forward
+  and backward kernel sequence is issued by ONE C++ call (ops/block.py ->
+  csrc/bindings/conv_bn_ops.cpp block_fwd / block_bwd); SyncBN statistics are exchanged
+  by the native communicator inside that call (the fused xGMI exchange by default:
+  reduce + exchange + finalize in one launch per BN);
+* global average pooling is a native kernel (pool.hip) and the projection head one
+  autograd node whose GEMMs run on the same MFMA kernels with bias/ReLU epilogues
+  (ops/head.py); the per-op path below (``fused=False``) remains as a reference executor.
 
 Reference forward: networks/resnet_big.py:57-67 (Bottleneck), 24-35 (BasicBlock),
 110-118 (ResNet), 177-181 (SupConResNet).
