@@ -24,6 +24,10 @@ namespace {
 #ifndef SDX_EW_UNROLL
 #define SDX_EW_UNROLL 1
 #endif
+// rows per trip of the column reduction's row loop (col_reduce_kernel); 4 = round-2 code
+#ifndef SDX_CR_UNROLL
+#define SDX_CR_UNROLL 8
+#endif
 
 // slab [rows][NS][C] fp32 -> sums [NS][C] fp64 in one launch. grid (ceil(C/64), gy): block
 // (x, y) sums its contiguous row range for 64 channels (4 thread rows, fp64) into
@@ -121,16 +125,20 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
 #pragma unroll
   for (int q = 0; q < NS; ++q) acc[q] = 0.0;
   if (c < C) {
-    // 4 rows per trip: 4·NS independent loads in flight per thread (latency-bound loop)
+    // SDX_CR_UNROLL rows per trip: that many x NS independent loads in flight per thread. The
+    // loop is latency-bound (the slab was just written by a conv epilogue on other CUs /
+    // XCDs), so the trip count, not the bytes, sets its time: 8 rows per trip halves the
+    // trips of the former 4.
+    constexpr int U = SDX_CR_UNROLL;
     int r = r0 + ty;
-    for (; r + 12 < r1; r += 16) {
-      float v[4][NS];
+    for (; r + 4 * (U - 1) < r1; r += 4 * U) {
+      float v[U][NS];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int q = 0; q < NS; ++q) v[u][q] = slab[((size_t)(r + 4 * u) * NS + q) * C + c];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int q = 0; q < NS; ++q) acc[q] += (double)v[u][q];
     }
