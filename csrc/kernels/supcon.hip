@@ -61,19 +61,22 @@ __device__ __forceinline__ void split_hi_lo(float x, uint16_t& hi, uint16_t& lo)
 }
 
 // LDS image of the 32 staged other rows (bf16 hi and lo images). D >= 128: unpadded
-// 2D-byte rows with the 16-B chunk index XOR-swizzled by sw(r) = ((r & 7) << 1) | (r >> 3 & 1):
-//   * tile-product ds_read_b128 (16 lanes = 16 consecutive rows, one chunk): 16 distinct
-//     slots of the 256-B bank row;
-//   * backward ds_read_b64_tr_b16 (32 lanes = 8 consecutive rows x 2 adjacent chunks):
-//     sw maps rows 0..7 to distinct even (8..15 to odd) values, so 16 distinct slots;
-//   * staging writes (16 lanes = the 16 chunks of one row): a bijection per row.
-// (The earlier +16-B row padding left 2-way conflicts on the transposed reads and 4-way on
-// the staging writes: ~50 % LDS bank conflicts at N = 8192, profiles/pmc_conv_supcon_r1_v2.txt.)
+// 2D-byte rows with the 16-B chunk index XOR-swizzled by sw(r) = (r & 7) << 1, chosen for
+// the three access patterns and their lane groups (MI355X_MICROARCH.md §LDS):
+//   * tile-product ds_read_b128 (groups {0–3,12–15,20–27}, ...: rows c of one 16-row tile,
+//     chunk k for h = 0 and k|1 for h = 1): each group hits all 16 slots of the 256-B row;
+//   * backward ds_read_b64_tr_b16 (32-lane halves: 8 rows x 2 adjacent chunks): sw/2 is a
+//     permutation of the 8 rows, so 16 distinct slots;
+//   * staging ds_write_b128 (8 contiguous lanes = 8 consecutive chunks of one row, banks mod
+//     128 B): distinct slots for any sw.
+// (Round 2's +16-B row padding: 2-way conflicts on the staging writes, ~50 % of LDS cycles
+// at N = 8192, profiles/pmc_conv_supcon_r1_v2.txt; a first swizzle with a row-bit-3 term in
+// bit 0 fixed the writes but left the b128 reads 2-way: 28-40 %, profiles/pmc_supcon_r3.txt.)
 // D = 64 keeps the padded rows.
 template <int D>
 __device__ __forceinline__ int sc_off(int row, int byte) {
   if constexpr (D >= 128) {
-    const int sw = ((row & 7) << 1) | ((row >> 3) & 1);
+    const int sw = (row & 7) << 1;
     return row * (D * 2) + ((((byte >> 4) ^ sw)) << 4) + (byte & 15);
   } else {
     return row * (D * 2 + 16) + byte;

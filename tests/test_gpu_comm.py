@@ -102,8 +102,10 @@ def test_native_executor_syncbn_path(gpu, name, which, kind, W):
     for a, b in ((b0, b1), (n0, n1)):
         for (na, ma), (_, mb) in zip(a.named_modules(), b.named_modules()):
             if isinstance(ma, torch.nn.BatchNorm2d):
+                # running_var is updated with the UNBIASED variance: n/(n-1) over the global
+                # row count, which differs between 1 and W ranks
                 assert torch.equal(ma.running_mean, mb.running_mean), na
-                assert torch.equal(ma.running_var, mb.running_var), na
+                assert torch.allclose(ma.running_var, mb.running_var, rtol=1e-3), na
     worst, bad, seen = (0.0, ""), [], 0
     for tag, a, b in (("blk", b0, b1), ("next", n0, n1)):
         for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
