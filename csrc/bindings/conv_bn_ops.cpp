@@ -50,6 +50,14 @@ void in_bn_ptrs(const OptT& sc, const OptT& sh, int64_t C, const float** ps, con
 // compute-bound (long K); short-K (memory-bound) GEMMs favour its higher occupancy.
 // Calibrated with tools/conv_bench.py --cfg 0..3 on the ResNet-50 shapes.
 int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
+  // SDX_CONV_CFG=c pins the fwd/dgrad tile config (tests): the BN-statistics epilogue's per-tile
+  // fp32 partial sums then cover the same rows whatever the per-rank batch, so a W-rank step
+  // reproduces the single-rank statistics bit for bit (tests/test_gpu_dist.py)
+  static const int pinned = [] {
+    const char* e = getenv("SDX_CONV_CFG");
+    return e != nullptr ? atoi(e) : -1;
+  }();
+  if (fill && pinned >= 0 && pinned <= 5) return pinned;
   const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
   const bool long_k = Kdim == 0 || Kdim > 256;
   const double pen_long[4] = {1.0, 1.04, 1.04, 1.35}, pen_short[4] = {1.0, 1.0, 1.0, 1.05};

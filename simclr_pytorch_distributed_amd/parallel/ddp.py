@@ -33,8 +33,11 @@ from . import comm
 
 
 class GradBucketReducer:
-    def __init__(self, flat, bucket_mb: float = 24.0, group=None, enabled: Optional[bool] = None,
+    def __init__(self, flat, bucket_mb: Optional[float] = None, group=None, enabled: Optional[bool] = None,
                  broadcast_init: bool = True):
+        if bucket_mb is None:
+            import os
+            bucket_mb = float(os.environ.get("SDX_BUCKET_MB", "24"))
         self.flat = flat
         self.group = group
         self.world = comm.world_size() if group is None else dist.get_world_size(group)

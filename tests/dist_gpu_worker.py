@@ -22,7 +22,7 @@ def main():
     name = os.environ.get("SDX_TEST_MODEL", "resnet18")
     G = 32                                    # global images (16 per rank at W=2: 32 views, so
     #                                           ResNet-50 layer 1 folds its BN3 on every rank)
-    argv = ["--model", name, "--backend", "native", "--dist_backend", "gloo", "--synthetic",
+    argv = ["--model", name, "--backend", os.environ.get("SDX_TEST_BACKEND", "native"), "--dist_backend", "gloo", "--synthetic",
             "--synthetic_size", "64", "--learning_rate", "0.05", "--grad_semantics", "exact",
             "--work_dir", out_dir, "--batch_size", str(G), "--ngpu", str(world)]
     if world > 1:
@@ -40,7 +40,7 @@ def main():
     per = G // world
     sl = slice(rank * per, (rank + 1) * per)
     x = torch.cat([imgs[0, sl], imgs[1, sl]]).cuda()
-    feats = eng.runner.forward(to_nhwc_input(x))
+    feats = eng.runner.forward(to_nhwc_input(x) if eng.backend == "native" else x)
     loss = eng.criterion(feats)
     eng.optimizer.zero_grad()
     loss.backward()

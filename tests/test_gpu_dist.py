@@ -2,7 +2,14 @@
 both processes on cuda:0) — SyncBN through the fused blocks, row-owned contrastive loss
 with gathered negatives, bucketed gradient reduction on the comm stream, fused SGD —
 must reproduce the single-rank step on the concatenated batch (exact gradient
-semantics), up to bf16 reduction-order noise."""
+semantics), up to bf16 reduction-order noise.
+
+The fwd/dgrad tile config is pinned (SDX_CONV_CFG=4) in every run: the auto choice depends
+on the GEMM's row count, i.e. on the per-rank batch, and the BN-statistics epilogue's
+fp32 per-tile partial sums then cover different rows. That alone perturbs the statistics
+at the fp32-ulp level, and ResNet-50 at random init amplifies forward perturbations
+chaotically (W=2 vs W=1 median parameter-gradient difference 0.61 unpinned vs 0.012
+pinned; torch's own autocast path: 1.25 — profiles/multirank_r50_r3.txt)."""
 import os
 import subprocess
 import sys
@@ -20,7 +27,7 @@ def _launch(world, out, syncbn_comm="", model="resnet18"):
     procs = []
     for r in range(world):
         env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, SDX_TEST_MODEL=model, RANK=str(r), LOCAL_RANK="0",
-                   WORLD_SIZE=str(world),
+                   WORLD_SIZE=str(world), SDX_CONV_CFG="4",
                    MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD="file://" + rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -71,6 +78,10 @@ def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, model, syncbn_co
     assert len(worst) == (163 if model == "resnet50" else 64)
     assert rel < 2e-3, rel
     assert torch.allclose(a["rm"], ref["rm"], rtol=1e-2, atol=1e-3)
-    assert worst[0][0] < 2e-2, worst[:8]
+    med = sorted(r for r, _ in worst)[len(worst) // 2]
+    assert med < 2e-2, med
+    # worst: ResNet-18 any parameter < 2e-2; ResNet-50 < 4e-2 — its stem BN bias gradient (a sum
+    # of 65536 bf16 terms that nearly cancel) moves 2.3 % with the reduction order alone
+    assert worst[0][0] < (4e-2 if model == "resnet50" else 2e-2), worst[:8]
     # global loss = sum of the ranks' row-owned losses
     assert abs(a["loss"] + b["loss"] - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3

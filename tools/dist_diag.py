@@ -4,8 +4,10 @@ runs the worker at W=1 and W=2 (both processes on cuda:0, gloo process group) un
 given environment overrides and prints the parameter-update difference and the parameters
 whose gradients differ most.
 
-python tools/dist_diag.py MODEL SYNCBN_COMM "ENV1" "ENV2"
-  ENV1 / ENV2: space-separated VAR=value overrides for the W=1 / W=2 runs ("" = none)
+python tools/dist_diag.py MODEL SYNCBN_COMM "ENV1" "ENV2" [W2]
+  ENV1 / ENV2: space-separated VAR=value overrides for the W=1 / second runs ("" = none);
+  W2 = world size of the second run (default 2; 1 compares two single-rank runs, e.g. a
+  summation-order perturbation such as SDX_STAT_FUSE=3: the chaos floor of the network)
 """
 import os
 import subprocess
@@ -37,13 +39,14 @@ def main():
     model, comm = sys.argv[1], sys.argv[2]
     env1 = dict(kv.split("=", 1) for kv in sys.argv[3].split()) if len(sys.argv) > 3 else {}
     env2 = dict(kv.split("=", 1) for kv in sys.argv[4].split()) if len(sys.argv) > 4 else {}
+    w2 = int(sys.argv[5]) if len(sys.argv) > 5 else 2
     with tempfile.TemporaryDirectory() as d1, tempfile.TemporaryDirectory() as d2:
         launch(1, d1, model, "", env1)
-        launch(2, d2, model, comm, env2)
+        launch(w2, d2, model, comm, env2)
         ref = torch.load(os.path.join(d1, f"{model}_w1_r0.pt"), weights_only=True)
-        a = torch.load(os.path.join(d2, f"{model}_w2_r0.pt"), weights_only=True)
+        a = torch.load(os.path.join(d2, f"{model}_w{w2}_r0.pt"), weights_only=True)
     rel = float((ref["flat"] - a["flat"]).norm() / ref["flat"].norm())
-    print(f"{model} comm={comm or 'gloo'} env1={env1} env2={env2}: param-update rel {rel:.4g}, "
+    print(f"{model} W=1 vs W={w2} comm={comm or 'gloo'} env1={env1} env2={env2}: param-update rel {rel:.4g}, "
           f"loss w1 {ref['loss']:.5f}")
     rows = []
     for n, o, k in zip(a["names"], a["offsets"], a["numels"]):
