@@ -3,6 +3,7 @@
 # 128 images per GPU, per-shape conv table, step profile. Crash / timeout ends the script.
 mkdir -p gpurun_out/r3s3
 cd "${GRAFT_REPO_ROOT:-.}"
+timeout -k 10 400 python -u -m pytest tests/test_gpu_dist.py -v --timeout 300 --timeout-method thread > gpurun_out/r3s3/dist_tests.txt 2>&1; rc=$?; [ $rc -le 1 ] || exit $rc
 bash tools/gpu/ab_bench.sh 3 "base:" "cr4:SDX_EXT_VARIANT=cr4" > gpurun_out/r3s3/ab_cr.txt 2>&1 || exit 1
 for pg in 256 128; do
   for kind in none fused emu; do
