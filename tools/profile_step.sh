@@ -12,5 +12,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /tmp/pp -o run -- python3 
 python tools/rocpd_to_csv.py /tmp/pp > /dev/null
 d=$(dirname $(find /tmp/pp -name "run_kernel_trace.csv" | head -1))
 python tools/rocprof_summary.py $d --steps 16 > $O/summary.txt
-python tools/step_timeline.py $d > $O/timeline.txt
+python tools/step_timeline.py $d --dump $O/step_kernels.txt > $O/timeline.txt
 grep -v amdgpu.ids $O/phases.txt | tail -25; head -30 $O/summary.txt; head -12 $O/timeline.txt

@@ -20,15 +20,20 @@ def main():
     if not dbs:
         sys.exit(f"no .db under {d}")
     rows = []
+    extra = []
     for db in dbs:
         c = sqlite3.connect(db)
-        rows += c.execute("select name, start, end, vgpr_count, accum_vgpr_count, lds_size, grid_x, workgroup_x "
-                          "from kernels order by start").fetchall()
+        cols = [x[0] for x in c.execute("select * from kernels limit 1").description]
+        # stream / queue ids when the schema has them (per-stream timelines, tools/step_timeline.py)
+        extra = [k for k in ("stream_id", "queue_id") if k in cols]
+        rows += c.execute("select name, start, end, vgpr_count, accum_vgpr_count, lds_size, grid_x, workgroup_x" +
+                          "".join(", " + k for k in extra) + " from kernels order by start").fetchall()
     rows.sort(key=lambda r: r[1])
     with open(os.path.join(d, "run_kernel_trace.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "VGPR_Count", "Accum_VGPR_Count",
-                    "LDS_Block_Size", "Grid_Size", "Workgroup_Size"])
+                    "LDS_Block_Size", "Grid_Size", "Workgroup_Size"] +
+                   [{"stream_id": "Stream_Id", "queue_id": "Queue_Id"}[k] for k in extra])
         w.writerows(rows)
     agg = defaultdict(lambda: [0, 0])
     for r in rows:

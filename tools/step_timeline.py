@@ -3,7 +3,9 @@
 (sgd_kernel end to sgd_kernel end), GPU-busy time (union of kernel intervals over all
 streams) and idle gaps, plus the busiest kernels of that step.
 
-python tools/step_timeline.py <rocprof dir>
+python tools/step_timeline.py <rocprof dir> [--dump FILE]
+  --dump: every kernel of that step (start / end in us from the step start, stream or
+  queue id, grid, name) for offline analysis
 """
 import csv
 import glob
@@ -47,6 +49,12 @@ def main():
         print(f"  {g:7.1f} @{at:8.1f}  {pn.split('(')[0]}  ->  {nn.split('(')[0]}")
     # per-stream busy time in the step (union per stream) and their overlap
     key = next((k for k in ("Stream_Id", "Queue_Id", "Stream_ID", "Queue_ID") if k in rows[0]), None)
+    if "--dump" in sys.argv:
+        with open(sys.argv[sys.argv.index("--dump") + 1], "w") as fo:
+            for r in rows[a + 1:b + 1]:
+                fo.write(f"{(int(r['Start_Timestamp']) - t0) / 1e3:9.1f} {(int(r['End_Timestamp']) - t0) / 1e3:9.1f} "
+                         f"{r.get(key, '-') if key else '-':>4} {r.get('Grid_Size', ''):>8} "
+                         f"{r['Kernel_Name'].split('(')[0].replace('void ', '')[:90]}\n")
     if key:
         by = defaultdict(list)
         for r in rows[a + 1:b + 1]:
