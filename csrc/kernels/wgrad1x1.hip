@@ -35,12 +35,18 @@ constexpr int W1_PF = 4;        // steps of loads in flight (register ring of 4 
 typedef __attribute__((address_space(3))) bf16x4 w1_lds_bf16x4;
 
 __device__ __attribute__((aligned(16))) uint16_t w1_zero16[8];
+typedef const __attribute__((address_space(1))) uint16_t* w1_gptr;
 
-// K-outer image [32][COLS] bf16: 16-B chunk ch of row r (igemm.hip kout_off, COLS >= 128)
+// K-outer image [rows][COLS] bf16: 16-B chunk ch of row r (igemm.hip kout_off, COLS >= 128);
+// the chunk XOR depends on row bits 0, 1 and 3 only
+template <int COLS>
+__device__ __forceinline__ int kout_swz_w1(int r) {
+  static_assert(COLS >= 128, "swizzle spans 16 chunks");
+  return ((r & 3) | (((r >> 3) & 1) << 2)) << 1;
+}
 template <int COLS>
 __device__ __forceinline__ int w1_off(int r, int ch) {
-  const int swz = ((r & 3) | (((r >> 3) & 1) << 2)) << 1;
-  return r * (COLS * 2) + ((ch ^ swz) << 4);
+  return r * (COLS * 2) + ((ch ^ kout_swz_w1<COLS>(r)) << 4);
 }
 
 struct W1Params {
@@ -208,7 +214,194 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_kernel(W1Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fragment-pipelined variant (default; SDX_W1_PIPE=0 restores the loop above). Above, every
+// step waits after its barrier for its own fragment reads (LDS latency under load) before
+// the first MFMA, and both waves of a SIMD leave the barrier together, so that latency and
+// the step's ds_write transfers are exposed once per 32 pixels (~32 % MFMA-busy on the
+// layer-3 shapes). Here the LDS ring has THREE buffers and the fragments are
+// double-buffered in registers: iteration k reads step k+1's fragments (stored one
+// iteration earlier, visible since the last barrier), runs step k's MFMAs on the fragments
+// read during iteration k-1, and stores step k+2 from the register ring into the buffer
+// step k-1 vacated — one barrier per step, no LDS latency in front of the MFMAs. (An
+// LDS-DMA version of this kernel, 3-stage ring of 64-pixel steps, measured 12-48 % slower
+// per kernel: profiles/ablate_wgrad_r3.txt.)
+template <int BN>
+__global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
+  constexpr int A_BYTES = 32 * W1_BM * 2;
+  constexpr int STAGE = A_BYTES + 32 * BN * 2;
+  constexpr int A_CPR = W1_BM / 8, B_CPR = BN / 8;
+  constexpr int NCH = 32 * (A_CPR + B_CPR) / W1_NT;
+  static_assert(NCH == 2 || NCH == 3, "loader layout");
+  constexpr int WN_COLS = BN / 4, TN = WN_COLS / 16;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[3 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h4 = lane >> 4, c16 = lane & 15;
+  const int wm = wv >> 2, wn = wv & 3;
+
+  const int tiles = p.k_tiles * p.c_tiles;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lin % tiles, split = lin / tiles;
+  const int k0 = (tile / p.c_tiles) * W1_BM, c0 = (tile % p.c_tiles) * BN;
+  const int s_begin = split * p.steps_per_split;
+  const int s_end = min(p.steps_total, s_begin + p.steps_per_split);
+
+  // loader: chunk u of this thread (u < NCH) is a dy chunk (pixel f/16 of the 32-pixel
+  // step, channel chunk f%16 of the 128 rows) for f = tid + 512u < 512, else an x chunk;
+  // chunk 0 is always dy, chunks 1 and 2 always x. Sources are 32-bit element offsets plus a
+  // uniform (scalar) step offset (host check: P·K, P·C < 2^31); past s_end the zero page,
+  // whose address lives in an SGPR pair the compiler cannot rematerialise (else it re-runs
+  // s_getpc + a GOT load + lgkmcnt(0) — draining the in-flight fragment reads — per select)
+  static_assert(32 * A_CPR == W1_NT, "chunk 0 = dy, chunks 1.. = x");
+  const int a_off = (tid / A_CPR) * p.K + k0 + (tid % A_CPR) * 8;
+  const int a_dst = w1_off<W1_BM>(tid / A_CPR, tid % A_CPR);
+  const int e1 = tid, e2 = tid + W1_NT;   // x chunk indices of chunks 1, 2
+  const int x_off1 = (e1 / B_CPR) * p.C + c0 + (e1 % B_CPR) * 8;
+  const int x_off2 = (e2 / B_CPR) * p.C + c0 + (e2 % B_CPR) * 8;
+  const int x_dst1 = A_BYTES + w1_off<BN>(e1 / B_CPR, e1 % B_CPR);
+  const int x_dst2 = A_BYTES + w1_off<BN>(e2 / B_CPR, e2 % B_CPR);
+  const int sA = 32 * p.K, sB = 32 * p.C;
+  w1_gptr zp = (w1_gptr)w1_zero16;
+  asm volatile("" : "+s"(zp));
+  const w1_gptr gdy = (w1_gptr)p.dy, gx = (w1_gptr)p.x;
+  // native vectors (a HIP uint4 read through an address-space-1 pointer becomes a memcpy
+  // that keeps the ring in scratch)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  struct Regs {
+    u32x4 a, b, c;
+  };
+  Regs r0, r1, r2, r3;
+  auto slot = [&](auto S) __attribute__((always_inline)) -> Regs& {
+    if constexpr (decltype(S)::value == 0) return r0;
+    else if constexpr (decltype(S)::value == 1) return r1;
+    else if constexpr (decltype(S)::value == 2) return r2;
+    else return r3;
+  };
+  typedef const __attribute__((address_space(1))) u32x4* g16;
+  auto load = [&](int step, Regs& r) __attribute__((always_inline)) {
+    const bool ok = step < s_end;
+    r.a = *(g16)(ok ? gdy + (a_off + step * sA) : zp);
+    r.b = *(g16)(ok ? gx + (x_off1 + step * sB) : zp);
+    if constexpr (NCH == 3) r.c = *(g16)(ok ? gx + (x_off2 + step * sB) : zp);
+  };
+  auto store = [&](unsigned char* sb, const Regs& r) __attribute__((always_inline)) {
+    *reinterpret_cast<u32x4*>(sb + a_dst) = r.a;
+    *reinterpret_cast<u32x4*>(sb + x_dst1) = r.b;
+    if constexpr (NCH == 3) *reinterpret_cast<u32x4*>(sb + x_dst2) = r.c;
+  };
+
+  const int q = c16 >> 2, pp = c16 & 3;
+  const int p_lo = 8 * h4 + q;   // fragment pixel rows p_lo and p_lo + 4
+  auto kout = [&](auto cols_tag, int row, int col0) __attribute__((always_inline)) {
+    constexpr int COLS = decltype(cols_tag)::value;
+    const int col = col0 + 4 * pp;
+    return w1_off<COLS>(row, col >> 3) + (col & 7) * 2;
+  };
+  // pixel row p_hi = p_lo + 4 differs from p_lo in row bit 2 only, which the swizzle
+  // ignores: its fragment half sits a constant 4 rows further (an immediate ds_read offset)
+  int ao[4], bo[TN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ao[i] = kout(std::integral_constant<int, W1_BM>{}, p_lo, wm * 64 + 16 * i);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bo[j] = A_BYTES + kout(std::integral_constant<int, BN>{}, p_lo, wn * WN_COLS + 16 * j);
+  auto frag = [&](const unsigned char* b, int o, auto cols_tag) __attribute__((always_inline)) -> bf16x8 {
+    constexpr int COLS = decltype(cols_tag)::value;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w1_lds_bf16x4*)(b + o));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w1_lds_bf16x4*)(b + o + 4 * COLS * 2));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  f32x4 acc[4][TN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment register sets (named, selected at compile time by step parity)
+  bf16x8 fa0[4], fb0[TN], fa1[4], fb1[TN];
+  auto read_frags = [&](const unsigned char* b, bf16x8 (&fa)[4], bf16x8 (&fb)[TN]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = frag(b, bo[j], std::integral_constant<int, BN>{});
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag(b, ao[i], std::integral_constant<int, W1_BM>{});
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[TN]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  };
+
+  // LDS buffers of steps k, k+1, k+2 (rotating)
+  unsigned char* b_cur = smem;
+  unsigned char* b_nxt = smem + STAGE;
+  unsigned char* b_st = smem + 2 * STAGE;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  // iteration for step k = base + U: read step k+1's fragments, MFMAs of step k, store step
+  // k+2 (ring slot (U+2)%4) into the buffer step k-1 vacated, refill that slot with k+6
+  auto iter = [&](int b0, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    using S = std::integral_constant<int, (u + 2) % 4>;
+    if constexpr ((u & 1) == 0) {
+      read_frags(b_nxt, fa1, fb1);
+      mfmas(fa0, fb0);
+    } else {
+      read_frags(b_nxt, fa0, fb0);
+      mfmas(fa1, fb1);
+    }
+    store(b_st, slot(S{}));
+    load(b0 + u + 6, slot(S{}));
+    __syncthreads();
+    unsigned char* t = b_cur;
+    b_cur = b_nxt;
+    b_nxt = b_st;
+    b_st = t;
+  };
+  load(s_begin, r0);
+  load(s_begin + 1, r1);
+  load(s_begin + 2, r2);
+  load(s_begin + 3, r3);
+  store(b_cur, r0);
+  store(b_nxt, r1);
+  load(s_begin + 4, r0);
+  load(s_begin + 5, r1);
+  __syncthreads();
+  read_frags(b_cur, fa0, fb0);
+  for (int b0 = s_begin; b0 < s_end; b0 += 4) {
+    iter(b0, I0{});
+    iter(b0, I1{});
+    iter(b0, I2{});
+    iter(b0, I3{});
+  }
+
+  float* out = p.part + (size_t)split * p.K * p.C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = k0 + wm * 64 + 16 * i + c16;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = c0 + wn * WN_COLS + 16 * j + 4 * h4;
+      const f32x4 a = acc[i][j];
+      st16<SDX_NT_PART != 0>(out + (size_t)m * p.C + n,
+                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                        __float_as_uint(a[3])));
+    }
+  }
+}
+
 int wgrad1x1_bn(const ConvGeom& g) { return g.C % 256 == 0 ? 256 : 128; }
+
+bool w1_pipe_enabled(const ConvGeom& g) {
+  static const bool on = [] {
+    const char* e = getenv("SDX_W1_PIPE");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const long P = (long)g.N * g.H * g.W;   // 32-bit element offsets
+  return on && P * g.K < (1L << 31) && P * g.C < (1L << 31);
+}
 
 }  // namespace
 
@@ -239,8 +432,14 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   if (!direct && partial == nullptr) return hipErrorInvalidValue;
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W1_NT);
-  if (bn == 256) hipLaunchKernelGGL(wgrad1x1_kernel<256>, grid, block, 0, s, p);
-  else hipLaunchKernelGGL(wgrad1x1_kernel<128>, grid, block, 0, s, p);
+  if (w1_pipe_enabled(g)) {
+    if (bn == 256) hipLaunchKernelGGL(wgrad1x1_pipe_kernel<256>, grid, block, 0, s, p);
+    else hipLaunchKernelGGL(wgrad1x1_pipe_kernel<128>, grid, block, 0, s, p);
+  } else if (bn == 256) {
+    hipLaunchKernelGGL(wgrad1x1_kernel<256>, grid, block, 0, s, p);
+  } else {
+    hipLaunchKernelGGL(wgrad1x1_kernel<128>, grid, block, 0, s, p);
+  }
   SDX_LAUNCH_CHECK();
   if (direct) return hipSuccess;
   return launch_splitk_reduce(partial, p.splits, (long)g.K * g.C / 4, dw, accumulate, s);

@@ -107,11 +107,14 @@ def test_wgrad3x3_tap_reuse(gpu, shape, splits):
     assert torch.equal(dw2, dw)
 
 
-@pytest.mark.parametrize("shape", [(4, 16, 256, 128), (2, 8, 512, 256), (8, 4, 128, 512), (3, 8, 384, 128)])
+@pytest.mark.parametrize("shape", [(4, 16, 256, 128), (2, 8, 512, 256), (8, 4, 128, 512), (3, 8, 384, 128),
+                                   (6, 4, 256, 128), (16, 16, 256, 256)])
 @pytest.mark.parametrize("splits", [1, 3, 0])
 def test_wgrad1x1_stream(gpu, shape, splits):
-    """Stride-1 1x1 wgrad kernel (cfg 10, wgrad1x1.hip) vs fp32 torch: 128- and 256-wide
-    column tiles, direct / split-K / auto split, accumulation into a sink, auto dispatch."""
+    """Stride-1 1x1 wgrad kernels (cfg 10, wgrad1x1.hip) vs fp32 torch: 128- and 256-wide
+    column tiles, direct / split-K / auto split, accumulation into a sink, auto dispatch.
+    Pixel counts that are multiples of 64 run the LDS-DMA kernel, (6, 4, ...) = 96 pixels
+    the register-staged one."""
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
     N, H, C, K = shape

@@ -15,7 +15,7 @@ def main():
         run = os.path.relpath(f, root).split(os.sep)[0].rsplit(".", 1)[0]
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if not any(t in k for t in ("igemm", "supcon", "splitk", "col_reduce", "wgrad3x3")):
+            if not any(t in k for t in ("igemm", "supcon", "splitk", "col_reduce", "wgrad")):
                 continue
             name = k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
             name = k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
