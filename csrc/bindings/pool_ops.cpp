@@ -36,6 +36,37 @@ torch::Tensor maxpool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, in
   return dx;
 }
 
+// max-pool forward + per-window first-max positions (uint8, same shape as y)
+std::vector<torch::Tensor> maxpool_fwd_idx(torch::Tensor x, int64_t k, int64_t stride, int64_t pad) {
+  check_nhwc(x, "x");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0 && pad < k && k * k <= 255, "bad pool geometry");
+  c10::DeviceGuard dg(x.device());
+  auto y = torch::empty({N, P, Q, C}, x.options());
+  auto idx = torch::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  check_hip(launch_maxpool_fwd_idx(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C, P, Q, k, stride,
+                                   pad, cur_stream()),
+            "maxpool_fwd_idx");
+  return {y, idx};
+}
+
+// max-pool backward from the recorded positions: dx [N, H, W, C]
+torch::Tensor maxpool_bwd_idx(torch::Tensor idx, torch::Tensor dy, int64_t H, int64_t W, int64_t k, int64_t stride,
+                              int64_t pad) {
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.sizes() == dy.sizes(),
+              "idx: contiguous uint8 of dy's shape");
+  TORCH_CHECK((H + 2 * pad - k) / stride + 1 == dy.size(1) && (W + 2 * pad - k) / stride + 1 == dy.size(2),
+              "pool geometry mismatch");
+  c10::DeviceGuard dg(dy.device());
+  auto dx = torch::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  check_hip(launch_maxpool_bwd_idx(idx.data_ptr<uint8_t>(), dy.data_ptr(), dx.data_ptr(), dy.size(0), H, W,
+                                   dy.size(3), dy.size(1), dy.size(2), k, stride, pad, cur_stream()),
+            "maxpool_bwd_idx");
+  return dx;
+}
+
 torch::Tensor gap_fwd(torch::Tensor x) {
   check_nhwc(x, "x");
   c10::DeviceGuard dg(x.device());
@@ -62,6 +93,10 @@ torch::Tensor gap_bwd(torch::Tensor dy, int64_t H, int64_t W) {
 void register_pool(pybind11::module& m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("maxpool_fwd_idx", &maxpool_fwd_idx, "max-pool forward + per-window first-max positions (uint8)");
+  m.def("maxpool_bwd_idx", &maxpool_bwd_idx, "max-pool backward from the recorded positions",
+        pybind11::arg("idx"), pybind11::arg("dy"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("k"),
+        pybind11::arg("stride"), pybind11::arg("pad"));
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
 }

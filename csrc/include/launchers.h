@@ -238,6 +238,12 @@ hipError_t launch_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C
                               int pad, hipStream_t s);
 hipError_t launch_maxpool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int H, int W, int C,
                               int P, int Q, int k, int stride, int pad, hipStream_t s);
+// forward that also records each window's first-max position (uint8 [N][P][Q][C], k*k <= 255)
+// and the backward that scatters from it (no re-read of the pooled input)
+hipError_t launch_maxpool_fwd_idx(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q,
+                                  int k, int stride, int pad, hipStream_t s);
+hipError_t launch_maxpool_bwd_idx(const uint8_t* idx, const void* dy, void* dx, int N, int H, int W, int C, int P,
+                                  int Q, int k, int stride, int pad, hipStream_t s);
 hipError_t launch_gap_fwd(const void* x, float* y, int N, int HW, int C, hipStream_t s);
 hipError_t launch_gap_bwd(const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
 

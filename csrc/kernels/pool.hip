@@ -31,8 +31,11 @@ struct PoolGeom {
   int N, H, W, C, P, Q, k, stride, pad;
 };
 
+// IDX: also store, per window and channel, the position (ddy·k + ddx) of its FIRST maximum
+// in scan order (uint8 [N][P][Q][C]); the backward then needs neither x nor y
+template <bool IDX>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
-                                                          PoolGeom g, long total8) {
+                                                          uint8_t* __restrict__ idx, PoolGeom g, long total8) {
   const int C8 = g.C / 8;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
     const int c8 = (int)(e % C8);
@@ -41,8 +44,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     const int p = (int)(r % g.P);
     const int n = (int)(r / g.P);
     float m[8];
+    int at[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) m[i] = -INFINITY;
+    for (int i = 0; i < 8; ++i) {
+      m[i] = -INFINITY;
+      at[i] = 0;
+    }
     for (int dy = 0; dy < g.k; ++dy) {
       const int yy = p * g.stride - g.pad + dy;
       if (yy < 0 || yy >= g.H) continue;
@@ -52,10 +59,56 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
         float v[8];
         unpack8(reinterpret_cast<const uint4*>(x)[(((long)n * g.H + yy) * g.W + xx) * C8 + c8], v);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], v[i]);
+        for (int i = 0; i < 8; ++i) {
+          if (IDX && v[i] > m[i]) at[i] = dy * g.k + dx;   // strict: the first maximum wins
+          m[i] = fmaxf(m[i], v[i]);
+        }
       }
     }
     reinterpret_cast<uint4*>(y)[e] = pack8(m);
+    if constexpr (IDX) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo |= (uint32_t)at[i] << (8 * i);
+        hi |= (uint32_t)at[4 + i] << (8 * i);
+      }
+      reinterpret_cast<uint2*>(idx)[e] = make_uint2(lo, hi);
+    }
+  }
+}
+
+// dx[n,h,w,c] = Σ over windows (p,q) containing (h,w) whose stored first-max position is
+// (h,w): dy[n,p,q,c] — windows in (p, q) order, the same sums as the recomputing kernel
+// below, from 8 B of index + 16 B of dy per window instead of re-reading its 9 inputs
+__global__ __launch_bounds__(256) void maxpool_bwd_idx_kernel(const uint8_t* __restrict__ idx,
+                                                              const uint16_t* __restrict__ dy,
+                                                              uint16_t* __restrict__ dx, PoolGeom g, long total8) {
+  const int C8 = g.C / 8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(e % C8);
+    long r = e / C8;
+    const int w = (int)(r % g.W); r /= g.W;
+    const int h = (int)(r % g.H);
+    const int n = (int)(r / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int p_lo = max(0, (h + g.pad - g.k + g.stride) / g.stride), p_hi = min(g.P - 1, (h + g.pad) / g.stride);
+    const int q_lo = max(0, (w + g.pad - g.k + g.stride) / g.stride), q_hi = min(g.Q - 1, (w + g.pad) / g.stride);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const long oi = (((long)n * g.P + p) * g.Q + q) * C8 + c8;
+        const uint2 iv = reinterpret_cast<const uint2*>(idx)[oi];
+        float gv[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[oi], gv);
+        const uint32_t pos = (uint32_t)((h - (p * g.stride - g.pad)) * g.k + (w - (q * g.stride - g.pad)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t at = ((i < 4 ? iv.x : iv.y) >> (8 * (i & 3))) & 0xffu;
+          if (at == pos) acc[i] += gv[i];
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[e] = pack8(acc);
   }
 }
 
@@ -153,8 +206,29 @@ hipError_t launch_maxpool_fwd(const void* x, void* y, int N, int H, int W, int C
                               int pad, hipStream_t s) {
   PoolGeom g{N, H, W, C, P, Q, k, stride, pad};
   const long total8 = (long)N * P * Q * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total8)), dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y, g,
-                     total8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total8)), dim3(256), 0, s, (const uint16_t*)x,
+                     (uint16_t*)y, nullptr, g, total8);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_maxpool_fwd_idx(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q,
+                                  int k, int stride, int pad, hipStream_t s) {
+  if (k * k > 255) return hipErrorInvalidValue;
+  PoolGeom g{N, H, W, C, P, Q, k, stride, pad};
+  const long total8 = (long)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total8)), dim3(256), 0, s, (const uint16_t*)x,
+                     (uint16_t*)y, idx, g, total8);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_maxpool_bwd_idx(const uint8_t* idx, const void* dy, void* dx, int N, int H, int W, int C, int P,
+                                  int Q, int k, int stride, int pad, hipStream_t s) {
+  PoolGeom g{N, H, W, C, P, Q, k, stride, pad};
+  const long total8 = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_idx_kernel, dim3(grid_for(total8)), dim3(256), 0, s, idx, (const uint16_t*)dy,
+                     (uint16_t*)dx, g, total8);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

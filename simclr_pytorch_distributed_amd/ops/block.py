@@ -262,19 +262,21 @@ class _Stem(torch.autograd.Function):
         cnt = (y.numel() // y.shape[-1]) * _world(group)
         sc, sh, mu, iv = _BN.forward(m, s, enc.bn1, cnt, training, group)
         a = m.bn_apply(y, sc, sh, None, None, None, 0, True)
-        out = m.maxpool_fwd(a, 3, 2, 1) if imagenet else a
+        # max-pool: its first-max positions (uint8) stand in for a and the pooled output in backward
+        out, idx = m.maxpool_fwd_idx(a, 3, 2, 1) if imagenet else (a, None)
         if training:
-            ctx.save_for_backward(x, y, a if imagenet else None, out if imagenet else None, mu, iv, sc, sh)
+            ctx.save_for_backward(x, y, idx, mu, iv, sc, sh)
             ctx.enc, ctx.group, ctx.params, ctx.cnt, ctx.geo = enc, group, params, cnt, (st, pad, imagenet)
+            ctx.hw = (a.shape[1], a.shape[2])
         return out
 
     @staticmethod
     def backward(ctx, dout):
         m = _ext.require()
-        x, y, a, out, mu, iv, sc, sh = ctx.saved_tensors
+        x, y, idx, mu, iv, sc, sh = ctx.saved_tensors
         st, pad, imagenet = ctx.geo
         dout = dout.contiguous()
-        da = m.maxpool_bwd(a, out, dout, 3, 2, 1) if imagenet else dout
+        da = m.maxpool_bwd_idx(idx, dout, ctx.hw[0], ctx.hw[1], 3, 2, 1) if imagenet else dout
         dy, _, _ = _bn_bwd(m, da, None, y, mu, iv, ctx.enc.bn1, ctx.cnt, ctx.group, mask=(sc, sh))
         w = ctx.enc.conv1.weight
         K, C, R, S = w.shape

@@ -8,17 +8,24 @@ from . import _ext
 
 
 class _MaxPool(torch.autograd.Function):
+    """The forward records each window's first-max position (uint8, a quarter of the pooled
+    input's bytes at 3x3/2); the backward scatters dy through it without re-reading the
+    input (profiles/cfg5_supcon224_kernels_r3.txt: the recomputing kernel was 5.3 ms of a
+    224x224 step)."""
+
     @staticmethod
     def forward(ctx, x, k, stride, pad):
-        y = _ext.require().maxpool_fwd(x, k, stride, pad)
-        ctx.save_for_backward(x, y)
-        ctx.cfg = (k, stride, pad)
+        if not ctx.needs_input_grad[0]:
+            return _ext.require().maxpool_fwd(x, k, stride, pad)
+        y, idx = _ext.require().maxpool_fwd_idx(x, k, stride, pad)
+        ctx.save_for_backward(idx)
+        ctx.cfg = (x.shape[1], x.shape[2], k, stride, pad)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y = ctx.saved_tensors
-        return _ext.require().maxpool_bwd(x, y, dy.contiguous(), *ctx.cfg), None, None, None
+        (idx,) = ctx.saved_tensors
+        return _ext.require().maxpool_bwd_idx(idx, dy.contiguous(), *ctx.cfg), None, None, None
 
 
 class _GlobalAvgPool(torch.autograd.Function):

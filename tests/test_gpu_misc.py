@@ -231,3 +231,31 @@ def test_stat_fuse_matches_column_reduce(gpu, name):
     # fp64 sums in another order: last-bit flips of the fp32 coefficients, compounded
     # through bf16 roundings block by block (same envelope as the dgrad-epilogue statistics)
     assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 15, 17, 16), (1, 8, 8, 8)])
+def test_maxpool_index_backward(gpu, shape):
+    """3x3/2 max-pool of the ImageNet stem: the forward's recorded first-max positions give
+    exactly the recomputing backward's gradient (ties included: bf16-rounded inputs tie
+    often), and both match torch's max_pool2d gradient on the same bf16 values."""
+    import torch.nn.functional as F
+    from simclr_pytorch_distributed_amd.ops import _ext
+    from simclr_pytorch_distributed_amd.ops.pool import maxpool_nhwc
+    m = _ext.require()
+    N, H, W, C = shape
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x = (torch.randn(N, H, W, C, device=gpu, generator=g) * 2).round().bfloat16()   # many exact ties
+    y0 = m.maxpool_fwd(x, 3, 2, 1)
+    y, idx = m.maxpool_fwd_idx(x, 3, 2, 1)
+    assert torch.equal(y, y0) and idx.dtype == torch.uint8 and int(idx.max()) <= 8
+    dy = torch.randn(y.shape, device=gpu, generator=g).bfloat16()
+    d_old = m.maxpool_bwd(x, y, dy, 3, 2, 1)
+    d_new = m.maxpool_bwd_idx(idx, dy, H, W, 3, 2, 1)
+    assert torch.equal(d_old, d_new)
+    xt = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    F.max_pool2d(xt, 3, 2, 1).backward(dy.float().permute(0, 3, 1, 2))
+    assert torch.allclose(d_new.float(), xt.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=1e-2)
+    # autograd path (ops/pool.py) uses the index kernels
+    xa = x.clone().requires_grad_(True)
+    maxpool_nhwc(xa).backward(dy)
+    assert torch.equal(xa.grad, d_new)
