@@ -151,9 +151,10 @@ StatFuse make_fuse(FuseReq& r, const torch::Tensor& like, int64_t M, int64_t Nco
   return f;
 }
 
+// no_out: statistics only, the output is not stored (first pass of a forward-folded BN3)
 std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad,
                                          bool want_stats, int64_t cfg, OptT in_scale, OptT in_shift,
-                                         FuseReq* fr, const GemmEpi* epi = nullptr) {
+                                         FuseReq* fr, const GemmEpi* epi = nullptr, bool no_out = false) {
   check_bf16_nhwc(x, "x");
   check_bf16_nhwc(w, "w");
   TORCH_CHECK(w.size(3) == x.size(3), "weight Cin != input C");
@@ -169,7 +170,8 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
   c10::DeviceGuard dg(x.device());
   const int64_t M = (int64_t)g.N * g.P * g.Q;
   if (cfg < 0) cfg = auto_cfg(M, g.K, (int64_t)g.R * g.S * g.C, true);
-  auto y = torch::empty({g.N, g.P, g.Q, g.K}, x.options());
+  TORCH_CHECK(!no_out || (want_stats && fr == nullptr && epi == nullptr), "statistics-only conv: stats, no epilogue");
+  auto y = no_out ? torch::Tensor() : torch::empty({g.N, g.P, g.Q, g.K}, x.options());
   torch::Tensor slab;
   float* sp = nullptr;
   if (want_stats) {
@@ -187,8 +189,8 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
     TORCH_CHECK(want_stats && isc == nullptr, "StatFuse: statistics without the BN prologue only");
     sf = make_fuse(*fr, x, M, g.K, (int)cfg, 2, lvl2);
   }
-  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), sp, (int)cfg, cur_stream(), isc, ish,
-                            epi, fr != nullptr ? &sf : nullptr),
+  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), no_out ? nullptr : y.data_ptr(), sp, (int)cfg, cur_stream(),
+                            isc, ish, epi, fr != nullptr ? &sf : nullptr),
             "conv_fwd");
   return {y, slab};
 }
@@ -199,7 +201,9 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
 torch::Tensor conv_fwd_bias(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, torch::Tensor bias,
                             bool relu) {
   check_vec(bias, w.size(0), "bias");
-  const GemmEpi epi{bias.data_ptr<float>(), relu ? 1 : 0, 0, 0};
+  GemmEpi epi{};
+  epi.bias = bias.data_ptr<float>();
+  epi.relu = relu ? 1 : 0;
   return conv_fwd_impl(x, w, stride, pad, false, -1, c10::nullopt, c10::nullopt, nullptr, &epi)[0];
 }
 
@@ -320,13 +324,21 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
                                                   int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
                                                   OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb,
                                                   OptT mb, OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub,
-                                                  FuseReq* fr, int store_masked = 0) {
-  check_bf16_nhwc(ya, "ya");
+                                                  FuseReq* fr, int store_masked = 0, int64_t extra_rows = 0) {
   const int64_t C = wt.size(0);
-  TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
+  // an empty ya: the BN input was never stored (forward-folded BN3) — the epilogue sums
+  // Σdz and Σdz·(0 − μ); the caller fills extra_rows rows of the slab with the Σdz·y terms
+  const bool no_y = !ya.defined() || ya.numel() == 0;
+  const int64_t elems = dy.size(0) * H * W * C;
+  if (!no_y) {
+    check_bf16_nhwc(ya, "ya");
+    TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
+  }
+  TORCH_CHECK(extra_rows >= 0 && (!no_y || (!yb.has_value() && !msc.has_value())),
+              "no-ya statistics: no second BN input, ReLU mask from bits");
   check_vec(ma, C, "ma");
   BnBwdStat bs{};
-  bs.ya = ya.data_ptr();
+  bs.ya = no_y ? nullptr : ya.data_ptr();
   bs.ma = ma.data_ptr<float>();
   if (yb.has_value()) {
     check_bf16_nhwc(*yb, "yb");
@@ -338,7 +350,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   }
   if (mask_bits.has_value()) {
     TORCH_CHECK(mask_bits->is_cuda() && mask_bits->scalar_type() == at::kByte && mask_bits->is_contiguous() &&
-                    mask_bits->numel() * 8 == ya.numel(),
+                    mask_bits->numel() * 8 == elems,
                 "mask_bits: uint8 [numel/8]");
     bs.mask = mask_bits->data_ptr<uint8_t>();
   } else if (msc.has_value()) {
@@ -358,7 +370,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) rows += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
   const int ns = yb.has_value() ? 3 : 2;
-  auto slab = torch::empty({rows, ns, C}, dy.options().dtype(at::kFloat));
+  auto slab = torch::empty({rows + extra_rows, ns, C}, dy.options().dtype(at::kFloat));
   bs.slab = slab.data_ptr<float>();
   TORCH_CHECK(!store_masked || (mask_bits.has_value() && stride == 1), "store_masked: stride-1 with a ReLU bitmask");
   bs.store_masked = store_masked;
@@ -370,9 +382,9 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
                                              int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
                                              OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb, OptT mb,
                                              OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0,
-                                             int store_masked = 0) {
+                                             int store_masked = 0, int64_t extra_rows = 0) {
   return conv_dgrad_bnstat_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, ya, ma, yb, mb, mask_bits,
-                                msc, msh, addend_sub, nullptr, store_masked);
+                                msc, msh, addend_sub, nullptr, store_masked, extra_rows);
 }
 
 }  // namespace
@@ -1125,14 +1137,21 @@ std::vector<torch::Tensor> fold_gram(torch::Tensor a2, int64_t side) {
   return fold_gram_now(a2);
 }
 
+// Gpre: G = dzᵀ·a2 already computed on the main stream (forward-folded BN3, whose backward
+// statistics need it first)
 void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const torch::Tensor& w3,
                      const torch::Tensor& coef, const torch::Tensor& sink, int64_t side,
-                     const torch::Tensor* gram = nullptr) {
+                     const torch::Tensor* gram = nullptr, const torch::Tensor* Gpre = nullptr) {
   const int64_t C3 = dz.size(3), K3 = a2.size(3);
   auto body = [&]() {
     auto opt = coef.options();
-    auto G = torch::empty({C3, 1, 1, K3}, opt);
-    conv_wgrad(dz, a2, 1, 1, 1, 0, 0, -1, G, false, c10::nullopt, c10::nullopt);
+    torch::Tensor G;
+    if (Gpre != nullptr) {
+      G = *Gpre;
+    } else {
+      G = torch::empty({C3, 1, 1, K3}, opt);
+      conv_wgrad(dz, a2, 1, 1, 1, 0, 0, -1, G, false, c10::nullopt, c10::nullopt);
+    }
     torch::Tensor Sm, cs, part;
     if (gram != nullptr) {
       Sm = gram[0];
@@ -1202,9 +1221,15 @@ std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor&
 // bn: [gamma, beta, running_mean, running_var] per BN, in the order bn1, bn2, (bn3), (shortcut bn)
 // returns [out, y1, a1, y2, a2|-, y3|-, ys|-, omask (uint8 ReLU bits of out; training only),
 //          then sc, sh, mu, iv per BN]
+//
+// fold_fwd (identity bottleneck, training; ops/block.py decides): the forward half of the BN3
+// fold — conv3 runs twice, first for its BN statistics only (nothing stored), then with the
+// BN3 apply + residual + ReLU + output bits in its epilogue, so y3 is never written nor
+// re-read (≈2 passes over the block's widest tensor); its backward takes Σdz·y3 from
+// W3 and dzᵀ·a2 (block_bwd, bnfold_rowdot) instead of re-reading y3
 std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor> w, std::vector<torch::Tensor> bn,
                                      int64_t stride, bool bottleneck, bool proj, bool training, double eps,
-                                     double momentum, int64_t comm) {
+                                     double momentum, int64_t comm, bool fold_fwd = false) {
   const int nconv = bottleneck ? 3 : 2;
   TORCH_CHECK((int)w.size() == nconv + (proj ? 1 : 0), "block_fwd: weight count");
   TORCH_CHECK(bn.size() == w.size() * 4, "block_fwd: 4 BN tensors per conv");
@@ -1220,19 +1245,40 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   st.push_back(c2.second);
   torch::Tensor last = c2.first, a2;
   int lastbn = 1;
-  if (bottleneck) {
-    a2 = bn_apply(c2.first, st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
-    auto c3 = conv_bn_fwd(a2, w[2], 1, 0, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm);
-    st.push_back(c3.second);
-    last = c3.first;
-    lastbn = 2;
-  }
+  fold_fwd = fold_fwd && bottleneck && !proj && training && stride == 1 && w[2].size(1) == 1 &&
+             w[2].size(2) == 1 && w[2].size(0) == x.size(3) && conv_fwd_bnapply_supported();
   torch::Tensor o, ys;
   // the block output's ReLU mask for backward: 1 bit per element instead of re-reading out
-  torch::Tensor omask = training ? torch::empty({last.numel() / 8}, last.options().dtype(at::kByte))
-                                 : torch::Tensor();
+  // (identity blocks: out has x's shape; projection / strided blocks: the last conv's)
+  torch::Tensor omask;
+  if (bottleneck) {
+    a2 = bn_apply(c2.first, st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
+    if (fold_fwd) {
+      // pass 1: BN3 statistics (nothing stored) -> finalize (SyncBN: fused exchange) ;
+      // pass 2: out = relu(bn3(y3) + x) and its bits straight from conv3's epilogue
+      auto c3s = conv_fwd_impl(a2, w[2], 1, 0, true, -1, c10::nullopt, c10::nullopt, nullptr, nullptr, true);
+      st.push_back(bn_forward(c3s[1], rows_of(a2), B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm));
+      omask = torch::empty({x.numel() / 8}, x.options().dtype(at::kByte));
+      GemmEpi epi{};
+      epi.bn_scale = st[2].sc.data_ptr<float>();
+      epi.bn_shift = st[2].sh.data_ptr<float>();
+      epi.resid = x.data_ptr();
+      epi.mask_out = omask.data_ptr<uint8_t>();
+      o = conv_fwd_impl(a2, w[2], 1, 0, false, -1, c10::nullopt, c10::nullopt, nullptr, &epi)[0];
+      last = torch::Tensor();
+    } else {
+      auto c3 = conv_bn_fwd(a2, w[2], 1, 0, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm);
+      st.push_back(c3.second);
+      last = c3.first;
+    }
+    lastbn = 2;
+  }
+  if (training && !omask.defined())
+    omask = torch::empty({last.numel() / 8}, last.options().dtype(at::kByte));
   const OptT om = training ? OptT(omask) : OptT();
-  if (proj) {
+  if (fold_fwd) {
+    // out computed by conv3's epilogue
+  } else if (proj) {
     auto cs = conv_bn_fwd(x, w[nconv], stride, 0, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
                           training, comm);
     st.push_back(cs.second);
@@ -1247,7 +1293,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   out[2] = a1;
   out[3] = c2.first;
   out[4] = bottleneck ? a2 : torch::Tensor();
-  out[5] = bottleneck ? last : torch::Tensor();
+  out[5] = bottleneck ? last : torch::Tensor();   // undefined with fold_fwd (y3 never stored)
   out[6] = ys;
   // layout: [out, y1, a1, y2, a2, y3, ys, omask, then sc, sh, mu, iv per BN]
   for (auto& b : st) {
@@ -1286,7 +1332,9 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   const int64_t H = x.size(1), W = x.size(2);
   const int lastbn = nconv - 1;
   const torch::Tensor& ylast = bottleneck ? y3 : y2;
-  const double cnt_last = rows_of(ylast), cnt1 = rows_of(y1);
+  // forward-folded BN3 (block_fwd fold_fwd): y3 was never stored
+  const bool no_y3 = bottleneck && (!y3.defined() || y3.numel() == 0);
+  const double cnt_last = rows_of(y2), cnt1 = rows_of(y1);   // conv3 is 1x1 stride 1: y3 rows = y2 rows
   torch::Tensor dylast, dys, dz;
   const bool have_slab = in_slab.has_value() && in_slab->defined() && in_slab->numel() > 0;
   if (have_slab) TORCH_CHECK(in_slab->size(1) == (proj ? 3 : 2), "block_bwd: in_slab set count");
@@ -1302,9 +1350,10 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   const bool fold = bottleneck && have_slab && nfw >= 1 && nfw <= (proj ? 2u : 1u) && fold_w[0].defined() &&
                     (nfw == 1 || (stride == 1 && fold_w[1].defined()));
   const bool fold_sc = fold && proj && nfw == 2;
+  TORCH_CHECK(!no_y3 || (fold && !proj), "block_bwd: a forward-folded block needs its BN3 fold (next block's slab)");
   const torch::Tensor* gram3 = grams ? &fold_w[nfw] : nullptr;
   const torch::Tensor* grams_sc = grams && nfw == 2 ? &fold_w[nfw + 2] : nullptr;
-  torch::Tensor coef3, coefs;
+  torch::Tensor coef3, coefs, Gfold;
   if (proj) {
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), G(nconv, 0),
@@ -1326,6 +1375,20 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
       dys = r[1];
     }
   } else {
+    if (no_y3) {
+      // Σdz·y3 = Σ_k W3[c][k]·(dzᵀ·a2)[c][k]: G on the main stream (the fold's wgrad reuses it),
+      // written into the two extra rows the next block's final dgrad left in in_slab
+      const int64_t C3 = dout.size(3), K3 = a2.size(3);
+      TORCH_CHECK(in_slab->size(0) > 2 && in_slab->size(2) == C3 && fold_w[0].size(0) == C3 &&
+                      fold_w[0].size(3) == K3,
+                  "block_bwd: forward-folded BN3 slab / weights");
+      Gfold = torch::empty({C3, 1, 1, K3}, dout.options().dtype(at::kFloat));
+      conv_wgrad(dout, a2, 1, 1, 1, 0, 0, -1, Gfold, false, c10::nullopt, c10::nullopt);
+      float* rows = in_slab->data_ptr<float>() + (in_slab->size(0) - 2) * 2 * C3;
+      check_hip(launch_bnfold_rowdot(Gfold.data_ptr<float>(), fold_w[0].data_ptr(), (int)C3, (int)K3, rows,
+                                     cur_stream()),
+                "bnfold_rowdot");
+    }
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), c10::nullopt,
                                     c10::nullopt, c10::nullopt, G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt)
@@ -1387,7 +1450,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     if (fold) {
       // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
       auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2, S(lastbn, 2), gram3);
-      side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3);
+      side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3, Gfold.defined() ? &Gfold : nullptr);
       AddPreScope pre;
       r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
     } else {
@@ -1417,9 +1480,13 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   auto last_dgrad = [&](OptT o, OptT add, OptT amask, int64_t asub = 0) -> torch::Tensor {
     if (!want_prev) return conv_dgrad(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, asub);
     const bool two = prev[2].defined() && prev[2].numel() > 0;
+    // the previous block folded its BN3 forward too (no y3): Σdz and −μ·Σdz here, two slab
+    // rows left for its Σdz·y3 (block_bwd no_y3)
+    const bool prev_noy = !prev[0].defined() || prev[0].numel() == 0;
+    TORCH_CHECK(!prev_noy || (prev_fold && !two), "block_bwd: previous block without y3 must fold");
     auto r = conv_dgrad_bnstat(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, prev[0], prev[1],
                                two ? OptT(prev[2]) : OptT(), two ? OptT(prev[3]) : OptT(), prev[4], c10::nullopt,
-                               c10::nullopt, asub, prev_fold ? 1 : 0);
+                               c10::nullopt, asub, prev_fold ? 1 : 0, prev_noy ? 2 : 0);
     prev_slab = r[1];
     return r[0];
   };
@@ -1544,7 +1611,7 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("ya"), pybind11::arg("ma"), pybind11::arg("yb") = pybind11::none(),
         pybind11::arg("mb") = pybind11::none(), pybind11::arg("mask_bits") = pybind11::none(),
         pybind11::arg("msc") = pybind11::none(), pybind11::arg("msh") = pybind11::none(),
-        pybind11::arg("addend_sub") = 0, pybind11::arg("store_masked") = 0);
+        pybind11::arg("addend_sub") = 0, pybind11::arg("store_masked") = 0, pybind11::arg("extra_rows") = 0);
   m.def("bn_bwd_coef_slab", &bn_bwd_coef_slab, "BN-backward coefficients (+dγ/dβ into sinks) from a dgrad stat slab",
         pybind11::arg("comm"), pybind11::arg("slab"), pybind11::arg("count"), pybind11::arg("g_a"),
         pybind11::arg("mean_a"), pybind11::arg("inv_a"), pybind11::arg("g_b") = pybind11::none(),
@@ -1554,7 +1621,7 @@ void register_conv_bn(pybind11::module& m) {
   m.def("block_fwd", &block_fwd, "native residual-block forward (whole kernel sequence; comm: SyncBN handle or 0)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bn"), pybind11::arg("stride"),
         pybind11::arg("bottleneck"), pybind11::arg("proj"), pybind11::arg("training"), pybind11::arg("eps"),
-        pybind11::arg("momentum"), pybind11::arg("comm") = 0);
+        pybind11::arg("momentum"), pybind11::arg("comm") = 0, pybind11::arg("fold_fwd") = false);
   m.def("fold_gram", &fold_gram,
         "BN3 fold: [a2ᵀ·a2, Σ_rows a2, scratch] of a folded conv's input, issued on the side stream",
         pybind11::arg("a2"), pybind11::arg("side"));

@@ -41,6 +41,8 @@ hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S
                                const void* w, int C, int K, float* sink, int accumulate, hipStream_t s);
 // cs[K] = column sums of a [rows][K] bf16 tensor (partial: [bnfold_colsum_blocks()][K] scratch)
 int bnfold_colsum_blocks();
+// two BN-backward slab rows [2][2][C] carrying Σ_k W[c][k]·G[c][k] (fp64 as fp32 hi + lo) in set 1
+hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, float* out_rows, hipStream_t s);
 hipError_t launch_bnfold_colsum(const void* x, long rows, int K, float* partial, float* cs, hipStream_t s);
 
 // ---- implicit-GEMM convolution (igemm.hip) ------------------------------------
@@ -76,7 +78,14 @@ struct GemmEpi {
   // DGRAD (stride 1): add the bf16 addend to the fp32 accumulators before the single bf16
   // rounding instead of after it (builds with SDX_ADD_PRE=1; BN3 fold experiment)
   int add_pre;
+  // FWD, stride-1 1x1 only: the block-output BatchNorm in the epilogue (forward-folded BN3) —
+  // out = relu(bf16(y)·bn_scale + bn_shift + resid) and its ReLU bits (1 bit per element)
+  const float* bn_scale;
+  const float* bn_shift;
+  const void* resid;
+  uint8_t* mask_out;
 };
+bool conv_fwd_bnapply_supported();
 int igemm_tile_m(int cfg);
 int igemm_tile_n(int cfg);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation

@@ -193,7 +193,34 @@ __global__ __launch_bounds__(256) void bnfold_wgrad_kernel(const float* __restri
   }
 }
 
+// forward-folded BN3 (its y = a2·Wᵀ never stored): Σ_rows dz·y per channel from the fold's
+// G = dzᵀ·a2 as Σ_k W[c][k]·G[c][k] (fp64), written as two extra rows of a BN-backward
+// statistics slab [2][2][C]: set 0 = 0, set 1 = the value split into fp32 hi + lo (the fp64
+// column reduction restores it); one wave per channel
+__global__ __launch_bounds__(64) void bnfold_rowdot_kernel(const float* __restrict__ G, const uint16_t* __restrict__ w,
+                                                           int C, int K, float* __restrict__ out) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  double acc = 0.0;
+  for (int k = lane; k < K; k += 64) acc += (double)bf2f(w[(size_t)c * K + k]) * (double)G[(size_t)c * K + k];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) {
+    const float hi = (float)acc, lo = (float)(acc - (double)hi);
+    out[c] = 0.f;
+    out[C + c] = hi;
+    out[2 * C + c] = 0.f;
+    out[3 * C + c] = lo;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, float* out_rows, hipStream_t s) {
+  if (C <= 0 || K <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_rowdot_kernel, dim3(C), dim3(64), 0, s, G, (const uint16_t*)w, C, K, out_rows);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
 
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
                               float* bias, const float* mu, const float* cs, long rows, hipStream_t s) {

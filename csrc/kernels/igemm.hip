@@ -96,6 +96,11 @@ struct IgemmParams {
   const float* bias;
   int relu, out_f32;
   int add_pre;   // GemmEpi::add_pre
+  // FWD VAR 2 (GemmEpi::bn_scale): the block-output BatchNorm applied in the epilogue —
+  // out = relu(bf16(y)·bn_sc + bn_sh + addend), its ReLU bits to mask_out (1 bit per element)
+  const float* bn_sc;
+  const float* bn_sh;
+  uint8_t* mask_out;
   // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
   int worder;
   // FWD statistics / DGRAD BN-backward statistics reduced in-kernel (sf.cnt != nullptr)
@@ -171,6 +176,19 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// ReLU bitmask byte of 8 packed bf16 (bit q: element q > 0), as bn.hip's apply kernel
+__device__ __forceinline__ uint32_t relu_bits8(uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo = w[q] & 0xffffu, hi = w[q] >> 16;
+    b |= (uint32_t)((lo & 0x7fffu) != 0 && !(lo & 0x8000u)) << (2 * q);
+    b |= (uint32_t)((hi & 0x7fffu) != 0 && !(hi & 0x8000u)) << (2 * q + 1);
+  }
+  return b;
 }
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
@@ -1026,6 +1044,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   static_assert(NT % CPR == 0 && CPR <= 64 && (BM * CPR) % NT == 0, "fixed column chunk per thread");
   const bool has_add = MODE == MODE_DGRAD && p.addend != nullptr && !(SDX_ADD_PRE && p.add_pre);
   constexpr bool bst = MODE == MODE_DGRAD && VAR != 0;
+  constexpr bool bnap = MODE == MODE_FWD && VAR == 2;   // block-output BN apply (+ residual, ReLU, bits)
   const int my_ch = tid % CPR, my_col = n0 + my_ch * 8;
   int eo[ITER];   // output element offset of each chunk (-1: outside the tensor)
   int ea[ITER];   // addend element offset (-1: no addend there)
@@ -1069,14 +1088,20 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       pf_add[sl] = ld16_stream(p.addend + (oa >= 0 ? oa : 0), oa >= 0);
       pf_am[sl] = (ok && p.addend_mask != nullptr) ? (uint32_t)p.addend_mask[o >> 3] : 0xffu;
     }
+    if constexpr (bnap) pf_add[sl] = ld16_stream(p.addend + (ok ? o : 0), ok);   // the residual
     if (MODE == MODE_DGRAD && bst) {
-      pf_ya[sl] = ld16_stream(reinterpret_cast<const uint16_t*>(p.bs.ya) + (ok ? o : 0), ok);
+      // ya == nullptr (a forward-folded BN3 whose y was never stored): y = 0, so the second
+      // sum is −μ·Σdz and the caller appends the Σdz·y rows (bnfold.hip rowdot)
+      const bool oky = ok && p.bs.ya != nullptr;
+      pf_ya[sl] = ld16_stream(reinterpret_cast<const uint16_t*>(p.bs.ya) + (oky ? o : 0), oky);
       const bool okb = ok && p.bs.yb != nullptr;
       pf_yb[sl] = ld16_stream(reinterpret_cast<const uint16_t*>(p.bs.yb) + (okb ? o : 0), okb);
       pf_bm[sl] = (ok && p.bs.mask != nullptr) ? (uint32_t)p.bs.mask[o >> 3] : 0xffu;
     }
   };
-  if (MODE == MODE_DGRAD && (has_add || bst)) {
+  // FWD without an output tensor: a statistics-only pass (forward-folded BN3, first pass)
+  const bool store_out = !(MODE == MODE_FWD && p.out == nullptr);
+  if ((MODE == MODE_DGRAD && (has_add || bst)) || bnap) {
     static_for<0, PF>([&](auto I) { prefetch(I, I); });
   }
 
@@ -1084,11 +1109,13 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   // at the same column of 16 consecutive rows hit distinct banks)
   constexpr int CRS = BN * 2 + 8;
   static_assert(BM * CRS <= LDS, "C tile must fit the staging LDS");
+  if (store_out) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      *reinterpret_cast<uint2*>(smem + (wm * WTM + 16 * i + c) * CRS + (wn * WTN + 16 * j + 4 * h) * 2) = ov[i][j];
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<uint2*>(smem + (wm * WTM + 16 * i + c) * CRS + (wn * WTN + 16 * j + 4 * h) * 2) = ov[i][j];
+  }
   __syncthreads();
   // fused BN-backward statistics (DGRAD): per-thread sums for column chunk my_ch
   const int bs_ns = p.bs.yb != nullptr ? 3 : 2;
@@ -1098,6 +1125,13 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     bmu_a[q] = bmu_b[q] = bmk_s[q] = bmk_t[q] = 0.f;
     bsum[0][q] = bsum[1][q] = bsum[2][q] = 0.f;
   }
+  float bsc[8], bsh[8];
+  if constexpr (bnap) {
+    if (my_col < p.Ncol) {
+      load8f(p.bn_sc + my_col, bsc);
+      load8f(p.bn_sh + my_col, bsh);
+    }
+  }
   if (MODE == MODE_DGRAD && bst && my_col < p.Ncol) {
     load8f(p.bs.ma + my_col, bmu_a);
     if (p.bs.yb) load8f(p.bs.mb + my_col, bmu_b);
@@ -1106,14 +1140,14 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       load8f(p.bs.msh + my_col, bmk_t);
     }
   }
-  {
+  if (store_out) {
     uint16_t* out = reinterpret_cast<uint16_t*>(p.out);
     static_for<0, ITER>([&](auto I) {
       constexpr int it = decltype(I)::value, sl = it % PF;
       const uint4 a_in = pf_add[sl], ya_in = pf_ya[sl], yb_in = pf_yb[sl];
       const uint32_t am = pf_am[sl], bm = pf_bm[sl];
       if constexpr (it + PF < ITER) {
-        if (MODE == MODE_DGRAD && (has_add || bst))
+        if ((MODE == MODE_DGRAD && (has_add || bst)) || bnap)
           prefetch(std::integral_constant<int, it + PF>{}, std::integral_constant<int, sl>{});
       }
       const int o = eo[it];
@@ -1144,6 +1178,22 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
             r[q] = pack_bf2(x0, x1);
           }
           v = make_uint4(r[0], r[1], r[2], r[3]);
+        }
+        if constexpr (bnap) {
+          // bn_apply mode 2 on the bf16-rounded conv output (the value y3 would have been
+          // stored as): the same operations in the same order, so the block output is the
+          // one the separate pass writes
+          float yv[8], rv[8];
+          unpack8(v, yv);
+          unpack8(a_in, rv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) yv[q] = yv[q] * bsc[q] + bsh[q];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) yv[q] += rv[q];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) yv[q] = fmaxf(yv[q], 0.f);
+          v = pack8(yv);
+          if (p.mask_out != nullptr) p.mask_out[o >> 3] = (uint8_t)relu_bits8(v);
         }
         // VAR 2 stores once, after the ReLU-backward mask below
         if (VAR != 2 || !(MODE == MODE_DGRAD && bst)) st16<SDX_NT_STORE != 0>(out + o, v);
@@ -1357,6 +1407,18 @@ int igemm_one() {
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   const dim3 g(grid), b(64 * WM * WN);
+  if (MODE == MODE_FWD && p.bn_sc != nullptr) {
+    // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
+    if constexpr (MODE == MODE_FWD && DEPTH == 3) {
+      if (p.Kdim <= BK && igemm_one())
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, true>), g, b, 0, s, p);
+      else
+        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, false>), g, b, 0, s, p);
+      SDX_LAUNCH_CHECK();
+      return hipSuccess;
+    }
+    return hipErrorInvalidValue;
+  }
   if (bs && p.bs.store_masked) {
     // masked-store statistics variant (projection head, BN3 fold): LDS-DMA tiles only
     if constexpr (MODE == MODE_DGRAD && DEPTH == 3) {
@@ -1500,6 +1562,10 @@ void set_epi(IgemmParams& p, const GemmEpi* epi) {
   p.relu = epi->relu;
   p.out_f32 = epi->out_f32;
   p.add_pre = epi->add_pre;
+  p.bn_sc = epi->bn_scale;
+  p.bn_sh = epi->bn_shift;
+  p.mask_out = epi->mask_out;
+  if (epi->resid != nullptr) p.addend = reinterpret_cast<const uint16_t*>(epi->resid);
 }
 }  // namespace
 
@@ -1513,6 +1579,13 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
     p.sf = *sf;
   }
   if (p.out_f32 && stats != nullptr) return hipErrorInvalidValue;
+  // BN-apply epilogue: stride-1 1x1 geometry (the residual shares the output rows), no
+  // statistics / fp32 output / bias; statistics-only pass: y == nullptr needs stats
+  if (p.bn_sc != nullptr &&
+      (p.bn_sh == nullptr || p.addend == nullptr || stats != nullptr || p.out_f32 || p.bias != nullptr ||
+       p.relu || in_scale != nullptr || y == nullptr || g.R != 1 || g.S != 1 || g.stride != 1 || g.pad != 0))
+    return hipErrorInvalidValue;
+  if (y == nullptr && (stats == nullptr || p.bn_sc != nullptr)) return hipErrorInvalidValue;
   p.in_scale = in_scale;
   p.in_shift = in_shift;
   p.g = g;
@@ -1641,3 +1714,7 @@ hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }
+
+// the BN-apply epilogue runs on the LDS-DMA tiles (DEPTH 3), not the register-staged or
+// ring variants
+bool conv_fwd_bnapply_supported() { return igemm_glds() != 0 && !igemm_ring(); }

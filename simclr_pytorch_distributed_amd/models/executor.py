@@ -135,9 +135,11 @@ class ModelRunner:
         g = self.sync_group
         out = fb.stem(x, enc, wc, training, g)
         chain = fb.BlockChain()
-        for blk in enc.blocks():
-            out = fb.bottleneck(out, blk, wc, training, g, chain) if isinstance(blk, Bottleneck) else \
-                fb.basic(out, blk, wc, training, g, chain)
+        blocks = list(enc.blocks())
+        for i, blk in enumerate(blocks):
+            # every block but the last hands its output to a native block (forward BN3 fold)
+            out = fb.bottleneck(out, blk, wc, training, g, chain, next_native=i + 1 < len(blocks)) \
+                if isinstance(blk, Bottleneck) else fb.basic(out, blk, wc, training, g, chain)
         if training and self._nbt:
             torch._foreach_add_(self._nbt, 1)
         return global_avgpool_nhwc(out)

@@ -320,7 +320,7 @@ class _NativeBlock(torch.autograd.Function):
     itself, in place on the compute stream (0 = single-process statistics)."""
 
     @staticmethod
-    def forward(ctx, x, blk, wc, training, info, comm_h, link_in, link_out, *params):
+    def forward(ctx, x, blk, wc, training, info, comm_h, link_in, link_out, fold_fwd, *params):
         m = _ext.require()
         convs, bns, bottle, proj = info
         bn0 = bns[0]
@@ -328,7 +328,7 @@ class _NativeBlock(torch.autograd.Function):
         for bn in bns:
             bn_list += [bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var]
         r = m.block_fwd(x, [wc.fwd(cv) for cv in convs], bn_list, blk.stride, bottle, proj, training, bn0.eps,
-                        bn0.momentum, comm_h)
+                        bn0.momentum, comm_h, fold_fwd)
         out = r[0]
         if training:
             e = _empty(x)
@@ -341,10 +341,12 @@ class _NativeBlock(torch.autograd.Function):
             if link_out is not None:
                 nconv = 3 if bottle else 2
                 st = r[8:]
-                link_out.prev = [r[5] if bottle else r[3], st[4 * (nconv - 1) + 2],
+                # r[5] is None for a forward-folded BN3 (y3 never stored): the next block's final
+                # dgrad then leaves two slab rows for Σdz·y3 (block_bwd)
+                link_out.prev = [(r[5] if r[5] is not None else e) if bottle else r[3], st[4 * (nconv - 1) + 2],
                                  r[6] if proj else e, st[4 * nconv + 2] if proj else _empty_f(x), r[7]]
                 rows = r[0].shape[0] * r[0].shape[1] * r[0].shape[2]
-                if _fold_eligible(convs, bottle, proj, rows):
+                if fold_fwd or _fold_eligible(convs, bottle, proj, rows):
                     # BN3 fold: the next block's final dgrad stores dz = dout·[out > 0] (marker)
                     link_out.prev.append(_fold_marker(x))
                     ctx.fold = 2 if (proj and _fold_shortcut(convs, rows)) else 1
@@ -387,7 +389,7 @@ class _NativeBlock(torch.autograd.Function):
         if lin is not None:
             lin.slab = pslab if (pslab is not None and pslab.numel() > 0) else None
         sinks.notify(ctx.params)
-        return (dx, None, None, None, None, None, None, None) + (None,) * len(ctx.params)
+        return (dx, None, None, None, None, None, None, None, None) + (None,) * len(ctx.params)
 
 
 _EMPTY = {}
@@ -413,6 +415,11 @@ BN3_FOLD_ROWS_PER_K2 = float(os.environ.get("SDX_BN3_FOLD_ROWS_PER_K2", "2"))
 # with the accumulator pre-add the correction is not needed (full-batch worst 0.033 rel either
 # way) and Grams in backward are faster (12.53 vs 12.60 ms, profiles/bn3_fold_r2.txt)
 FOLD_GRAM_FWD = os.environ.get("SDX_FOLD_GRAM_FWD", "0") != "0"
+# forward half of the fold (block_fwd fold_fwd, default on): conv3 twice — BN3 statistics, then
+# BN3 + residual + ReLU in its epilogue — so y3 is never stored; Σdz·y3 in backward from
+# W3 and dzᵀ·a2. Needs the next block's dgrad statistics hand-off (SDX_DGRAD_BNSTAT)
+FOLD_FWD = os.environ.get("SDX_BN3_FOLD_FWD", "1") != "0"
+DGRAD_BNSTAT = os.environ.get("SDX_DGRAD_BNSTAT", "1") != "0"
 
 
 def _fold_eligible(convs, bottle, proj, rows) -> bool:
@@ -486,7 +493,21 @@ def block_params(mod) -> List[torch.nn.Parameter]:
     return list(info[1]) if info is not None else [p for p in mod.parameters()]
 
 
-def bottleneck(x, blk, wc, training: bool, group=None, chain: Optional[BlockChain] = None):
+def _fold_fwd(x, info, training, next_native) -> bool:
+    """Forward half of the BN3 fold (block_fwd fold_fwd): identity bottlenecks that fold their
+    BN3 backward AND whose successor is a native block (its final dgrad supplies the slab the
+    folded backward needs, since y3 is not kept)."""
+    convs, bns, bottle, proj = info
+    if not (FOLD_FWD and training and next_native and bottle and not proj and DGRAD_BNSTAT):
+        return False
+    rows = x.shape[0] * x.shape[1] * x.shape[2]
+    return convs[1].stride == (1, 1) and _fold_eligible(convs, bottle, proj, rows)
+
+
+def bottleneck(x, blk, wc, training: bool, group=None, chain: Optional[BlockChain] = None,
+               next_native: bool = False):
+    """``next_native``: the block that consumes this one's output is a native block too
+    (set by the executor for every block but the encoder's last)."""
     info, params = _block_info(blk)
     h = _native_comm(group, info)
     if h >= 0:
@@ -494,7 +515,8 @@ def bottleneck(x, blk, wc, training: bool, group=None, chain: Optional[BlockChai
         lout = BlockLink() if (chain is not None and training) else None
         if chain is not None:
             chain.last = lout
-        return _NativeBlock.apply(x, blk, wc, training, info, h, lin, lout, *params)
+        ff = lout is not None and _fold_fwd(x, info, training, next_native)
+        return _NativeBlock.apply(x, blk, wc, training, info, h, lin, lout, ff, *params)
     if chain is not None:
         chain.last = None
     return _Bottleneck.apply(x, blk, wc, training, group, *params)
@@ -508,7 +530,7 @@ def basic(x, blk, wc, training: bool, group=None, chain: Optional[BlockChain] = 
         lout = BlockLink() if (chain is not None and training) else None
         if chain is not None:
             chain.last = lout
-        return _NativeBlock.apply(x, blk, wc, training, info, h, lin, lout, *params)
+        return _NativeBlock.apply(x, blk, wc, training, info, h, lin, lout, False, *params)
     if chain is not None:
         chain.last = None
     return _Basic.apply(x, blk, wc, training, group, *params)

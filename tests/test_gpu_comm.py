@@ -89,8 +89,10 @@ def test_native_executor_syncbn_path(gpu, name, which, kind, W):
         nxt = getattr(mdl.encoder, lay)[int(idx) + 1]
         ninfo, nparams = block._block_info(nxt)
         link = block.BlockLink()
-        mid = block._NativeBlock.apply(xi, blk, wc, True, info, hh, None, link, *params)
-        out = block._NativeBlock.apply(mid, nxt, wc, True, ninfo, hh, link, None, *nparams)
+        # layer-1/2 identity bottlenecks also fold their BN3 forward (no y3; Σdz·y3 from W3, dzᵀa2)
+        ff = block._fold_fwd(xi, info, True, True)
+        mid = block._NativeBlock.apply(xi, blk, wc, True, info, hh, None, link, ff, *params)
+        out = block._NativeBlock.apply(mid, nxt, wc, True, ninfo, hh, link, None, False, *nparams)
         if dout is None:
             dout = torch.randn_like(out)
         out.backward(dout)

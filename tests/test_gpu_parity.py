@@ -144,8 +144,9 @@ def test_block_pairs_gradients_match_fp32(gpu, name, fold, monkeypatch):
         chain = fb.BlockChain()
         xn = xin.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).requires_grad_(True)
         out = xn
-        for blk in nb[i:i + 2]:
-            out = (fb.bottleneck if isinstance(blk, Bottleneck) else fb.basic)(out, blk, wc, True, None, chain)
+        for j, blk in enumerate(nb[i:i + 2]):
+            out = fb.bottleneck(out, blk, wc, True, None, chain, next_native=j == 0) if isinstance(blk, Bottleneck) \
+                else fb.basic(out, blk, wc, True, None, chain)
         dy = torch.randn(out.shape, generator=g).to(gpu).to(torch.bfloat16)
         out.backward(dy)
         torch.cuda.synchronize()
@@ -240,6 +241,58 @@ def test_trajectory_tracks_fp32(gpu):
         assert abs(mn[w] - mt[w]) <= tol, (w, mn[w], mt[w], mc[w])
 
 
+def test_bn3_fold_forward_matches(gpu, monkeypatch):
+    """Forward half of the BN3 fold (block_fwd fold_fwd: conv3 twice, BN3 + residual + ReLU in
+    its epilogue, y3 never stored; backward Σdz·y3 from W3 and dzᵀ·a2) vs the backward-only
+    fold on identity bottleneck pairs of ResNet-50 layers 1-2: the block outputs, their ReLU
+    bits and the BN running statistics are bit-identical (same conv, same statistics, the
+    apply's operations in the same order); every gradient agrees to bf16 noise (Σdz·y3 from
+    the unrounded y3)."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner
+    from simclr_pytorch_distributed_amd.ops import block as fb
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    monkeypatch.setattr(fb, "BN3_FOLD_ROWS_PER_K2", 0.0)
+    monkeypatch.setattr(fb, "BN3_FOLD", True)
+    nat_m, _ = _models(gpu, "resnet50")
+    flat = FlatParams(nat_m)
+    runner = ModelRunner(nat_m, "native", master=flat.flat)
+    wc = runner.weight_cache()
+    nb = list(nat_m.encoder.blocks())
+    g = torch.Generator().manual_seed(9)
+    for i in (1, 4, 5):
+        hw = 32 if i < 4 else 16
+        x = torch.randn(16, hw, hw, nb[i].conv1.in_channels, generator=g).relu().to(gpu).to(torch.bfloat16)
+        dy, res = None, {}
+        bufs = [t for j in (i, i + 1) for t in nb[j].buffers()]
+        snap = [t.clone() for t in bufs]
+        for ff in (False, True):
+            monkeypatch.setattr(fb, "FOLD_FWD", ff)
+            with torch.no_grad():   # both runs update the running statistics from the same state
+                for t, v in zip(bufs, snap):
+                    t.copy_(v)
+            flat.zero_grad()
+            wc.refresh()
+            chain = fb.BlockChain()
+            xn = x.clone().requires_grad_(True)
+            mid = fb.bottleneck(xn, nb[i], wc, True, None, chain, next_native=True)
+            out = fb.bottleneck(mid, nb[i + 1], wc, True, None, chain)
+            if dy is None:
+                dy = torch.randn(out.shape, generator=g).to(gpu).to(torch.bfloat16)
+            out.backward(dy)
+            torch.cuda.synchronize()
+            stats = [t.clone() for j in (i, i + 1) for t in nb[j].buffers()]
+            res[ff] = (mid.detach().clone(), out.detach().clone(), stats,
+                       [xn.grad.float().clone()] + [p.grad.float().clone() for j in (i, i + 1)
+                                                    for p in nb[j].parameters()])
+        assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1]), i
+        for a, b in zip(res[True][2], res[False][2]):
+            assert torch.equal(a, b), i
+        names = ["dx"] + [f"block {j} {n}" for j in (i, i + 1) for n, _ in nb[j].named_parameters()]
+        worst = max((float((a - b).norm() / (b.norm() + 1e-30)), n) for n, a, b in zip(names, res[True][3], res[False][3]))
+        print(f"block {i}: worst fold_fwd vs fold gradient rel {worst[0]:.3g} ({worst[1]})")
+        assert worst[0] < 2e-2, worst
+
+
 def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
     """BN3 fold (csrc/kernels/bnfold.hip) vs the materialised dy3 path on the same two-block
     chains (folding bottleneck -> next block) of ResNet-50 layers 1-2: every parameter
@@ -270,7 +323,8 @@ def test_bn3_fold_matches_unfolded(gpu, monkeypatch):
             wc.refresh()
             chain = fb.BlockChain()
             xn = x.clone().requires_grad_(True)
-            out = fb.bottleneck(fb.bottleneck(xn, nb[i], wc, True, None, chain), nb[i + 1], wc, True, None, chain)
+            out = fb.bottleneck(fb.bottleneck(xn, nb[i], wc, True, None, chain, next_native=True), nb[i + 1], wc, True,
+                                None, chain)
             if dy is None:
                 dy = torch.randn(out.shape, generator=g).to(gpu).to(torch.bfloat16)
             out.backward(dy)
@@ -366,8 +420,8 @@ def test_stage_gradients_match_fp32(gpu, fold, monkeypatch):
         chain = fb.BlockChain()
         xn = xin.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).requires_grad_(True)
         out = xn
-        for blk in sn:
-            out = fb.bottleneck(out, blk, wc, True, None, chain)
+        for j, blk in enumerate(sn):
+            out = fb.bottleneck(out, blk, wc, True, None, chain, next_native=j + 1 < len(sn))
         dy = torch.randn(out.shape, generator=g).to(gpu).to(torch.bfloat16)
         out.backward(dy)
         torch.cuda.synchronize()
