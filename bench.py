@@ -190,7 +190,8 @@ def main():
                        "global_batch": global_batch, "per_gpu_batch": per_gpu, "views": 2,
                        "image_size": size, "seq_len": None, "micro_batch_views": mb or None,
                        "parallelism": f"dp{n}" + ("+syncbn" if n > 1 and not a.no_syncbn else ""),
-                       "backend": eng.backend, "hip_graph": graphed, "views_per_sec": round(2 * value, 2),
+                       "backend": eng.backend, "syncbn_transport": eng.syncbn_transport, "hip_graph": graphed,
+                       "views_per_sec": round(2 * value, 2),
                        "peak_hbm_gb": round(peak_gb, 2), "hbm_capacity_gb": 288,
                        "last_loss_local": round(loss, 4)},
         }), flush=True)

@@ -98,9 +98,12 @@ class PretrainEngine:
             if self.backend == "torch":
                 from ..parallel.syncbn import convert_sync_bn
                 model = convert_sync_bn(model)
+                self.syncbn_transport = "torch-syncbn"
             else:
                 self.sync_group = dist.group.WORLD
                 self._setup_syncbn_comm(opt, dev)
+                if self.syncbn_transport == "none":
+                    self.syncbn_transport = "process-group"
         if world > 1 and self.backend == "native":
             self._setup_gather_comm(opt, dev)
         emu = int(os.environ.get("SDX_SYNCBN_EMU", "0") or 0)
@@ -113,6 +116,7 @@ class PretrainEngine:
             kind = os.environ.get("SDX_SYNCBN_EMU_KIND", "fused")
             h = m.xgmi_emu_small_comm(emu) if kind == "fused" else m.emu_small_comm(emu)
             comm.set_native_small_comm(self.sync_group, h)
+            self.syncbn_transport = f"emulated-{emu}-{kind}"
             logging.info(f"SyncBN emulated over {emu} virtual ranks ({kind})")
         model = model.to(dev)
         if dev.type == "cuda":
@@ -154,6 +158,10 @@ class PretrainEngine:
             self._resume(opt.resume)
 
     # ------------------------------------------------------------------------------
+    # SyncBN statistics transport actually in use (bench.py reports it): none (W=1),
+    # xgmi-fused, rccl-native, process-group (c10d collectives), emulated-W
+    syncbn_transport = "none"
+
     def _setup_syncbn_comm(self, opt, dev):
         """SyncBN statistics transport for the native backend.
 
@@ -177,6 +185,7 @@ class PretrainEngine:
                 self._xgmi = impl
                 comm.set_small_allreduce(None, impl)
                 comm.set_native_small_comm(None, impl.handle)
+                self.syncbn_transport = "xgmi-fused"
                 logging.info("SyncBN statistics: fused one-shot xGMI exchange (native executor)")
                 return
             except Exception as e:  # noqa: BLE001
@@ -187,6 +196,7 @@ class PretrainEngine:
             handle = comm.create_rccl_small_comm(None, timeout)
             if handle:
                 comm.set_native_small_comm(None, handle)
+                self.syncbn_transport = "rccl-native"
                 logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
             else:
                 logging.warning("SyncBN statistics use the process-group all-reduce")
