@@ -1227,15 +1227,47 @@ std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor&
 // BN3 apply + residual + ReLU + output bits in its epilogue, so y3 is never written nor
 // re-read (≈2 passes over the block's widest tensor); its backward takes Σdz·y3 from
 // W3 and dzᵀ·a2 (block_bwd, bnfold_rowdot) instead of re-reading y3
+//
+// side (optional HIP stream): a projection block's shortcut conv (+ its statistics slab) runs
+// there, concurrently with the main branch conv1 -> bn1 -> conv2 -> ...; its BN finalize (and
+// any SyncBN exchange) stays on the compute stream after the join, so exchanges keep one order
 std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor> w, std::vector<torch::Tensor> bn,
                                      int64_t stride, bool bottleneck, bool proj, bool training, double eps,
-                                     double momentum, int64_t comm, bool fold_fwd = false) {
+                                     double momentum, int64_t comm, bool fold_fwd = false, int64_t side = 0) {
   const int nconv = bottleneck ? 3 : 2;
   TORCH_CHECK((int)w.size() == nconv + (proj ? 1 : 0), "block_fwd: weight count");
   TORCH_CHECK(bn.size() == w.size() * 4, "block_fwd: 4 BN tensors per conv");
   auto B = [&](int i, int k) { return bn[i * 4 + k]; };
   std::vector<BnState> st;
   std::vector<torch::Tensor> out(7);
+  // shortcut conv on the side stream: outputs allocated on the compute stream (they are
+  // read there after the join), the side stream only writes them
+  torch::Tensor ys_side, slab_side;
+  hipEvent_t sc_done = nullptr;
+  if (proj && training && side != 0 && !stat_fuse_enabled(1)) {
+    const torch::Tensor& ws = w[nconv];
+    check_bf16_nhwc(x, "x");
+    check_bf16_nhwc(ws, "w_shortcut");
+    TORCH_CHECK(ws.size(3) == x.size(3) && ws.size(1) == 1 && ws.size(2) == 1, "block_fwd: 1x1 shortcut");
+    ConvGeom gs{};
+    gs.N = x.size(0); gs.H = x.size(1); gs.W = x.size(2); gs.C = x.size(3);
+    gs.K = ws.size(0); gs.R = gs.S = 1; gs.stride = stride; gs.pad = 0;
+    gs.P = (gs.H - 1) / stride + 1;
+    gs.Q = (gs.W - 1) / stride + 1;
+    const int64_t M = (int64_t)gs.N * gs.P * gs.Q;
+    const int cfg = auto_cfg(M, gs.K, gs.C, true);
+    ys_side = torch::empty({gs.N, gs.P, gs.Q, gs.K}, x.options());
+    slab_side = torch::empty({(M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg), 2, gs.K}, x.options().dtype(at::kFloat));
+    hipEvent_t fork = next_event();
+    hipStream_t ss = reinterpret_cast<hipStream_t>(side);
+    check_hip(hipEventRecord(fork, cur_stream()), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(ss, fork, 0), "hipStreamWaitEvent");
+    check_hip(launch_conv_fwd(gs, x.data_ptr(), ws.data_ptr(), ys_side.data_ptr(), slab_side.data_ptr<float>(), cfg,
+                              ss),
+              "block_fwd shortcut conv (side stream)");
+    sc_done = next_event();
+    check_hip(hipEventRecord(sc_done, ss), "hipEventRecord");
+  }
   const int64_t s1 = bottleneck ? 1 : stride, p1 = bottleneck ? 0 : 1;
   auto c1 = conv_bn_fwd(x, w[0], s1, p1, B(0, 0), B(0, 1), B(0, 2), B(0, 3), eps, momentum, training, comm);
   st.push_back(c1.second);
@@ -1279,10 +1311,17 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   if (fold_fwd) {
     // out computed by conv3's epilogue
   } else if (proj) {
-    auto cs = conv_bn_fwd(x, w[nconv], stride, 0, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
-                          training, comm);
-    st.push_back(cs.second);
-    ys = cs.first;
+    if (sc_done != nullptr) {
+      check_hip(hipStreamWaitEvent(cur_stream(), sc_done, 0), "hipStreamWaitEvent");
+      st.push_back(bn_forward(slab_side, rows_of(ys_side), B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps,
+                              momentum, training, comm));
+      ys = ys_side;
+    } else {
+      auto cs = conv_bn_fwd(x, w[nconv], stride, 0, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
+                            training, comm);
+      st.push_back(cs.second);
+      ys = cs.first;
+    }
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true, om);
   } else {
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, x, c10::nullopt, c10::nullopt, 2, true, om);
@@ -1621,7 +1660,8 @@ void register_conv_bn(pybind11::module& m) {
   m.def("block_fwd", &block_fwd, "native residual-block forward (whole kernel sequence; comm: SyncBN handle or 0)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bn"), pybind11::arg("stride"),
         pybind11::arg("bottleneck"), pybind11::arg("proj"), pybind11::arg("training"), pybind11::arg("eps"),
-        pybind11::arg("momentum"), pybind11::arg("comm") = 0, pybind11::arg("fold_fwd") = false);
+        pybind11::arg("momentum"), pybind11::arg("comm") = 0, pybind11::arg("fold_fwd") = false,
+        pybind11::arg("side") = 0);
   m.def("fold_gram", &fold_gram,
         "BN3 fold: [a2ᵀ·a2, Σ_rows a2, scratch] of a folded conv's input, issued on the side stream",
         pybind11::arg("a2"), pybind11::arg("side"));

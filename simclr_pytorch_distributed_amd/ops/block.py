@@ -327,8 +327,12 @@ class _NativeBlock(torch.autograd.Function):
         bn_list = []
         for bn in bns:
             bn_list += [bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var]
+        # a projection block's shortcut conv runs on the wgrad side stream (idle in forward)
+        from . import streams
+        side = streams.side(x.device).cuda_stream if (proj and training and SC_SIDE and streams.ENABLED and x.is_cuda) \
+            else 0
         r = m.block_fwd(x, [wc.fwd(cv) for cv in convs], bn_list, blk.stride, bottle, proj, training, bn0.eps,
-                        bn0.momentum, comm_h, fold_fwd)
+                        bn0.momentum, comm_h, fold_fwd, side)
         out = r[0]
         if training:
             e = _empty(x)
@@ -461,6 +465,9 @@ def _empty(like):
 
 
 NATIVE_EXEC = os.environ.get("SDX_NATIVE_EXEC", "1") != "0"
+# projection blocks: the shortcut conv runs on the (forward-idle) side stream, concurrently
+# with conv1 -> bn1 -> conv2 -> ...; its BN finalize stays on the compute stream
+SC_SIDE = os.environ.get("SDX_SC_SIDE", "1") != "0"
 
 
 def _block_info(blk):
