@@ -83,6 +83,40 @@ def test_native_engine_step(gpu, tmp_path):
     assert torch.isfinite(eng.flat.flat).all().item()
 
 
+@pytest.mark.parametrize("kind", ["fused", "emu"])
+def test_native_engine_step_emulated_syncbn(gpu, tmp_path, monkeypatch, kind):
+    """The whole native training step (ResNet-50: stem, every block incl. the BN3 folds and the
+    forward fold, head, loss, SGD) with SyncBN over 8 emulated ranks on this GPU
+    (SDX_SYNCBN_EMU=8; 'fused': the fused xGMI exchange kernel over 8 device-memory arenas,
+    'emu': reduce -> x8 -> finalize) vs the single-process step: the 8 virtual ranks hold
+    identical data, so the global statistics are exact multiples of the local ones and the
+    parameter update must match the single-process one."""
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    args = ["--batch_size", "64", "--synthetic", "--synthetic_size", "256", "--work_dir", str(tmp_path),
+            "--model", "resnet50", "--backend", "native"]
+    idx = torch.arange(64, device=gpu)
+    res = []
+    w0 = None
+    for emu in ("0", "8"):
+        monkeypatch.setenv("SDX_SYNCBN_EMU", emu)
+        monkeypatch.setenv("SDX_SYNCBN_EMU_KIND", kind)
+        eng = PretrainEngine(parse_pretrain(args, make_dirs=False))
+        assert eng.syncbn_transport == ("none" if emu == "0" else f"emulated-8-{kind}")
+        if w0 is None:
+            w0 = eng.flat.flat.clone()
+        else:
+            eng.flat.flat.copy_(w0)
+        st = eng.train_step(idx, 1, 0, 10)
+        torch.cuda.synchronize()
+        res.append((float(st["loss_local"]), eng.flat.flat.clone()))
+    (l0, p0), (l1, p1) = res
+    rel = float((p1 - p0).norm() / (p0 - w0).norm())
+    print(f"emulated 8-rank SyncBN ({kind}) vs single process: loss {l1:.6f} vs {l0:.6f}, update rel {rel:.3g}")
+    assert abs(l1 - l0) <= 1e-5 * abs(l0)
+    assert rel < 1e-4, rel
+
+
 def test_native_blocks_teacher_forced(gpu):
     """Each native block vs the torch block fed the same (bf16-rounded) input."""
     from simclr_pytorch_distributed_amd.models import executor as ex
