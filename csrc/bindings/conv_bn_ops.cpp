@@ -296,14 +296,9 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   // sub-pixel classes: each gets the taps r ≡ ph+pad, s ≡ pw+pad (mod stride)
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) {
-      int r0, nr, s0, ns, Hc, Wc;
-      conv_dgrad_class(g, ph, pw, &r0, &nr, &s0, &ns, &Hc, &Wc);
-      torch::Tensor wc;
-      if (nr > 0 && ns > 0)
-        wc = wt.slice(1, r0, g.R, stride).slice(2, s0, g.S, stride).contiguous();
-      else
-        wc = wt;   // no taps: the kernel writes zeros and never reads B
-      check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), add, (int)cfg,
+      // each class reads its taps straight from the full Wt (no per-class weight copy; a
+      // class without taps writes zeros and never reads B)
+      check_hip(launch_conv_dgrad_class(g, ph, pw, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
                                         cur_stream(), amask, bs, add ? (int)addend_sub : 0),
                 "conv_dgrad(class)");
       if (bs) bs->row0 += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);

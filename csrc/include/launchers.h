@@ -94,10 +94,11 @@ struct StatFuse;
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr,
                            const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);
-// strided dgrad = stride² sub-pixel classes; wt_cls = Wt[:, r0::st, s0::st, :] (contiguous)
+// strided dgrad = stride² sub-pixel classes; wt = the full Wt [C][R][S][K] (each class reads
+// its taps r0::st, s0::st in place)
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
 // addend (optional, may alias dx): bf16 tensor of dx's shape added in the epilogue
-hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
+hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                    const BnBwdStat* bstat = nullptr, int addend_sub = 0,
                                    const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);

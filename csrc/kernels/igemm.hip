@@ -106,6 +106,11 @@ struct IgemmParams {
   // FWD statistics / DGRAD BN-backward statistics reduced in-kernel (sf.cnt != nullptr)
   StatFuse sf;
   int M, Ncol, Kdim;
+  // FWD / DGRAD weight operand addressing: output column col, logical k = (kr, ks, kc) reads
+  // b[col·b_row + b_t0 + kr·b_tr + ks·b_ts + kc]. FWD W [K][R][S][Cp] and stride-1 DGRAD Wt
+  // [C][R][S][K] give b_row = Kdim and k itself; a strided DGRAD class reads its taps
+  // r = r0 + st·kr, s = s0 + st·ks straight from the full Wt (no per-class weight copies)
+  int b_row, b_t0, b_tr, b_ts;
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
   int ph, pw, Hc, Wc, r0, s0, nr, ns;
@@ -462,7 +467,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const int col = n0 + b_row(i);
-      b_off[i] = col < p.Ncol ? col * p.Kdim : -1;
+      b_off[i] = col < p.Ncol ? col * p.b_row : -1;
     }
     const int k = k_begin + kin_ch * 8;
     kc = k % cdim;
@@ -627,11 +632,12 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
         ra[i] = ld16_or_zero(p.a + off, ok);
       }
-      // B: weights [Ncol][Kdim] K-contiguous
+      // B: weights, 8 channels of one tap per chunk (b_row / b_t0 / b_tr / b_ts addressing)
+      const int kb = p.b_t0 + kr * p.b_tr + ks * p.b_ts + kc;
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + k + 8 <= p.b_elems);
-        rb[i] = ld16_or_zero(p.b + b_off[i] + k, kok && b_off[i] >= 0);
+        SDX_DCHECK(!(kok && b_off[i] >= 0) || (long)b_off[i] + kb + 8 <= p.b_elems);
+        rb[i] = ld16_or_zero(p.b + b_off[i] + kb, kok && b_off[i] >= 0);
       }
       // advance the k decode by one tile
       kc += BK;
@@ -738,11 +744,12 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
                                          (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
                                          16, 0, 0);
       }
+      const int kb = p.b_t0 + u_kr * p.b_tr + u_ks * p.b_ts + u_c0 + lane_c;
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
         const bool ok = kok && b_off[i] >= 0;
-        SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
+        SDX_DCHECK(!ok || (long)b_off[i] + kb + 8 <= p.b_elems);
+        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + kb) : zp;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                          16, 0, 0);
@@ -772,11 +779,12 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
                                        (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
                                        16, 0, 0);
     }
+    const int kb = p.b_t0 + kr * p.b_tr + ks * p.b_ts + kc;
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
       const bool ok = kok && b_off[i] >= 0;
-      SDX_DCHECK(!ok || (long)b_off[i] + k + 8 <= p.b_elems);
-      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + k) : zp;
+      SDX_DCHECK(!ok || (long)b_off[i] + kb + 8 <= p.b_elems);
+      const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + kb) : zp;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
                                        16, 0, 0);
@@ -1596,6 +1604,10 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
   p.M = g.N * g.P * g.Q;
   p.Ncol = g.K;
   p.Kdim = g.R * g.S * g.C;
+  p.b_row = p.Kdim;
+  p.b_t0 = 0;
+  p.b_tr = g.S * g.C;
+  p.b_ts = g.C;
   p.a_elems = (long)g.N * g.H * g.W * g.C;
   p.b_elems = (long)p.Ncol * p.Kdim;
   return launch_any<MODE_FWD>(p, cfg, s);
@@ -1618,7 +1630,7 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
   return (M + bm - 1) / bm;
 }
 
-hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt_cls, void* dx,
+hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
                                    const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi,
                                    const StatFuse* sf) {
@@ -1636,7 +1648,7 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   p.addend_mask = (const uint8_t*)addend_mask;
   p.g = g;
   p.a = (const uint16_t*)dy;
-  p.b = (const uint16_t*)wt_cls;
+  p.b = (const uint16_t*)wt;   // the full Wt [C][R][S][K]; the class's taps are strided into it
   p.out = dx;
   p.addend = (const uint16_t*)addend;
   p.ph = ph;
@@ -1646,8 +1658,12 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   if (p.M == 0) return hipSuccess;
   p.Ncol = g.C;
   p.Kdim = p.nr * p.ns * g.K;
+  p.b_row = g.R * g.S * g.K;
+  p.b_t0 = (p.r0 * g.S + p.s0) * g.K;
+  p.b_tr = g.stride * g.S * g.K;
+  p.b_ts = g.stride * g.K;
   p.a_elems = (long)g.N * g.P * g.Q * g.K;
-  p.b_elems = (long)p.Ncol * p.Kdim;
+  p.b_elems = (long)p.Ncol * p.b_row;
   return launch_any<MODE_DGRAD>(p, cfg, s);
 }
 
