@@ -35,7 +35,7 @@ from ..losses.supcon import DistributedContrastiveLoss
 from ..models.executor import ModelRunner
 from ..models.resnet import SupConResNet
 from ..ops import _ext
-from ..optim.flat import FlatParams, build_optimizer
+from ..optim.flat import FlatParams, FusedSGD, build_optimizer
 from ..optim.schedules import adjust_learning_rate, warmup_learning_rate
 from ..parallel import comm
 from ..parallel.ddp import GradBucketReducer
@@ -125,7 +125,16 @@ class PretrainEngine:
         self.flat = FlatParams(model)
         self.optimizer = build_optimizer(opt.optimizer, self.flat, opt.learning_rate, opt.momentum,
                                          opt.weight_decay, backend="torch" if self.backend == "torch" else "auto")
-        self.reducer = GradBucketReducer(self.flat) if world > 1 else None
+        # SDX_EARLY_STEP=1 (native SGD): each bucket's update runs as soon as its gradients are
+        # final (after its collective with several ranks), overlapping the rest of backward.
+        # Off by default: on one MI355X the step's tail shrinks by ~85 us but the update
+        # kernels slow the concurrent critical-path backward kernels more (12.31 -> 12.44-12.60
+        # ms/step same box, profiles/early_step_r3.txt)
+        early = None
+        if (isinstance(self.optimizer, FusedSGD) and self.optimizer.native and not getattr(opt, "cuda_graph", False)
+                and os.environ.get("SDX_EARLY_STEP", "0") == "1"):
+            early = self.optimizer.apply_range
+        self.reducer = GradBucketReducer(self.flat, early_step=early) if (world > 1 or early is not None) else None
         self.optimizer.grad_scale = (1.0 / world) if opt.grad_semantics == "ref" else 1.0
         self.runner = ModelRunner(model, self.backend, opt.precision, self.sync_group, master=self.flat.flat)
         self.criterion = DistributedContrastiveLoss(opt.method, opt.temp, opt.base_temperature, opt.contrast_mode,
@@ -280,6 +289,9 @@ class PretrainEngine:
             return self._step_body_gradcache(idx, epoch, it, mb)
         ph = self.prof.phase
         with ph("augment"):
+            prefetch = getattr(self.runner, "prefetch_weights", None)
+            if prefetch is not None:
+                prefetch()          # weight conversion overlaps the augmentation launch
             x = self.make_views(idx, epoch, it)
             labels = self.labels[idx]
         with ph("forward"):

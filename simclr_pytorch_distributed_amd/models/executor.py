@@ -127,6 +127,12 @@ class ModelRunner:
                          if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
         return self._wc
 
+    def prefetch_weights(self):
+        """Start this step's bf16 weight conversion on the side stream (native fused path)."""
+        if (self.backend == "native" and self.fused and self.master is not None
+                and os.environ.get("SDX_WPREP_PREFETCH", "1") != "0"):
+            self.weight_cache().prefetch()
+
     def _encode_fused(self, x, training):
         from ..ops import block as fb
         enc = self.model.encoder

@@ -59,9 +59,34 @@ class ConvWeightCache:
         self.native = ok and dev.type == "cuda" and _ext.available()
         self.segs = torch.tensor(rows, dtype=torch.int64, device=dev) if self.native else None
         self.version = -1
+        self._pending = None     # event of a prefetch() issued on the side stream
+
+    def prefetch(self):
+        """Issue the next :meth:`refresh` now on the side stream (after all work queued so far
+        on the current stream, i.e. the previous step's optimizer update), so the conversion
+        overlaps the step's augmentation launch; :meth:`refresh` then only waits for it.
+        Nothing the step reads before the first convolution depends on these weights."""
+        from . import streams
+        if not (self.native and streams.ENABLED):
+            return
+        dev = self.buf.device
+        main = torch.cuda.current_stream(dev)
+        s = streams.side(dev)
+        s.wait_stream(main)
+        with torch.cuda.stream(s):
+            _ext.require().wprep(self.master, self.buf, self.segs, self.max_tiles)
+        if getattr(self, "_ev", None) is None:
+            self._ev = torch.cuda.Event()
+        self._ev.record(s)
+        self._pending = self._ev
 
     def refresh(self):
-        """Re-derive all bf16 copies from the current fp32 master weights (one launch)."""
+        """Re-derive all bf16 copies from the current fp32 master weights (one launch), or
+        wait for the copy a :meth:`prefetch` already issued."""
+        if self._pending is not None:
+            torch.cuda.current_stream(self.buf.device).wait_event(self._pending)
+            self._pending = None
+            return
         if self.native:
             _ext.require().wprep(self.master, self.buf, self.segs, self.max_tiles)
         else:

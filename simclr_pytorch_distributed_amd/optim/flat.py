@@ -138,6 +138,16 @@ class FusedSGD(_FlatOptimizer):
         super().__init__(flat, lr, momentum, weight_decay)
         self.nesterov = nesterov
         self.native = backend != "torch" and flat.flat.is_cuda and _ext.available()
+        self._applied = []      # [start, end) slices updated early this step (apply_range)
+
+    @torch.no_grad()
+    def apply_range(self, start: int, end: int):
+        """Update the flat slice [start, end) now, on the current stream (the bucket reducer's
+        early step: its gradients are final); :meth:`step` then skips it. Native path only."""
+        f = self.flat
+        _ext.require().sgd_step(f.flat[start:end], f.grad[start:end], self.buf[start:end], self.lr_t, self.momentum,
+                                self.weight_decay, self.grad_scale, self.nesterov)
+        self._applied.append((start, end))
 
     @torch.no_grad()
     def step(self):
@@ -145,8 +155,15 @@ class FusedSGD(_FlatOptimizer):
         self._join()
         f = self.flat
         if self.native:
-            _ext.require().sgd_step(f.flat, f.grad, self.buf, self.lr_t, self.momentum, self.weight_decay,
-                                    self.grad_scale, self.nesterov)
+            m = _ext.require()
+            # the slices no early apply_range covered (all of it without a bucket reducer)
+            pos, n = 0, f.flat.numel()
+            for a, b in sorted(self._applied) + [(n, n)]:
+                if a > pos:
+                    m.sgd_step(f.flat[pos:a], f.grad[pos:a], self.buf[pos:a], self.lr_t, self.momentum,
+                               self.weight_decay, self.grad_scale, self.nesterov)
+                pos = max(pos, b)
+            self._applied = []
         else:
             d = f.grad * self.grad_scale
             if self.weight_decay:

@@ -20,7 +20,13 @@ reducer built on the flat gradient buffer of :class:`optim.flat.FlatParams`:
   through one ~153 GB/s link per step, i.e. ≈0.3 ms for 24 MiB — well under the
   backward time that follows each launch, and ≫ the ~20-40 µs fixed cost of a launch;
 * parameters/buffers are broadcast from rank 0 once at construction (one collective on
-  the flat buffer); the per-forward BN buffer broadcast of DDP is dropped.
+  the flat buffer); the per-forward BN buffer broadcast of DDP is dropped (SURVEY Q20);
+* ``early_step(start, end)`` (optional, e.g. :meth:`optim.flat.FusedSGD.apply_range`): the
+  optimizer update of a bucket's slice, issued on the communication stream right after
+  the bucket's collective (or, with one rank, as soon as its gradients are final), so the
+  elementwise update of the deeper layers runs while backward is still computing the
+  shallow ones and only the last bucket's update is left after backward (the whole-buffer
+  SGD pass was ~90 us at the end of the ResNet-50 step). Used with one rank as well.
 """
 from __future__ import annotations
 
@@ -34,14 +40,16 @@ from . import comm
 
 class GradBucketReducer:
     def __init__(self, flat, bucket_mb: Optional[float] = None, group=None, enabled: Optional[bool] = None,
-                 broadcast_init: bool = True):
+                 broadcast_init: bool = True, early_step=None):
         if bucket_mb is None:
             import os
             bucket_mb = float(os.environ.get("SDX_BUCKET_MB", "24"))
         self.flat = flat
         self.group = group
         self.world = comm.world_size() if group is None else dist.get_world_size(group)
-        self.enabled = (self.world > 1) if enabled is None else enabled
+        self.enabled = (self.world > 1) if enabled is None else enabled   # all-reduce the buckets
+        self.early_step = early_step
+        self.active = self.enabled or early_step is not None            # track bucket completion
         cap = int(bucket_mb * (1 << 20) / 4)
         # buckets in backward (= flat buffer) order
         self.buckets: List[dict] = []
@@ -50,7 +58,8 @@ class GradBucketReducer:
             start = flat.offsets[i]
             end = start + (flat.params[i].numel() + 4095) // 4096 * 4096
             if cur is None or (end - cur["start"]) > cap and cur["params"]:
-                cur = {"start": start, "end": end, "params": [], "ready": 0, "work": None, "idx": len(self.buckets)}
+                cur = {"start": start, "end": end, "params": [], "ready": 0, "work": None, "launched": False,
+                       "idx": len(self.buckets)}
                 self.buckets.append(cur)
             cur["params"].append(i)
             cur["end"] = end
@@ -59,7 +68,7 @@ class GradBucketReducer:
             for i in b["params"]:
                 self.bucket_of[i] = b_idx
         self.is_cuda = flat.grad.is_cuda
-        self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (self.is_cuda and self.enabled) else None
+        self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (self.is_cuda and self.active) else None
         self._hooks = []
         self._index = {id(p): i for i, p in enumerate(flat.params)}
         # a parameter is counted once per backward: fused blocks notify through their gradient
@@ -69,14 +78,14 @@ class GradBucketReducer:
         self._paused = False
         self._listener = None
         self.launch_log: List[int] = []     # bucket indices in launch order (tests, profiling)
-        if self.enabled:
+        if self.active:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
             # fused native blocks write gradients into their sinks directly and notify here
             from ..ops import sinks
             self._listener = sinks.add_listener(self._on_sink)
-            if broadcast_init:
-                self.broadcast_parameters()
+        if self.enabled and broadcast_init:
+            self.broadcast_parameters()
 
     def _on_sink(self, p):
         i = self._index.get(id(p))
@@ -107,6 +116,7 @@ class GradBucketReducer:
 
     def _launch(self, b):
         view = self.flat.grad[b["start"]:b["end"]]
+        b["launched"] = True
         if self.comm_stream is not None:
             ev = torch.cuda.current_stream().record_event()
             with torch.cuda.stream(self.comm_stream):
@@ -118,10 +128,22 @@ class GradBucketReducer:
                 from ..ops import streams
                 if streams.ENABLED:
                     self.comm_stream.wait_stream(streams.side(view.device))
-                b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+                if self.enabled:
+                    b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+                if self.early_step is not None:
+                    if b["work"] is not None:
+                        b["work"].wait()     # orders the comm stream after the collective
+                        b["work"] = None
+                    self.early_step(b["start"], b["end"])
             self.launch_log.append(b["idx"])
         else:
-            b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+            if self.enabled:
+                b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+            if self.early_step is not None:
+                if b["work"] is not None:
+                    b["work"].wait()
+                    b["work"] = None
+                self.early_step(b["start"], b["end"])
             self.launch_log.append(b["idx"])
 
     def no_sync(self):
@@ -140,17 +162,19 @@ class GradBucketReducer:
 
     def finish(self):
         """Wait for all bucket reductions (launching any bucket whose params got no grad)."""
-        if not self.enabled:
+        if not self.active:
             return
         if self.is_cuda:
             from ..ops import streams
             streams.join(self.flat.grad.device)
         for b in self.buckets:
-            if b["work"] is None:
+            if not b["launched"]:
                 self._launch(b)
         for b in self.buckets:
-            b["work"].wait()
+            if b["work"] is not None:
+                b["work"].wait()
             b["work"] = None
+            b["launched"] = False
             b["ready"] = 0
         self._seen = [False] * len(self._seen)
         if self.comm_stream is not None:

@@ -30,11 +30,12 @@ def test_row_normalize_matches_torch(gpu, D):
     assert torch.allclose(xa.grad.double(), xb.grad, rtol=1e-4, atol=1e-4 * xb.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("shape", [(512, 128), (300, 100), (8192, 128)])
 @pytest.mark.parametrize("momentum", [1.0, 0.9])
-def test_norm_stats_matches_torch(gpu, momentum):
+def test_norm_stats_matches_torch(gpu, momentum, shape):
     m = _m()
     torch.manual_seed(1)
-    x = torch.randn(512, 128, device=gpu) * 3
+    x = torch.randn(*shape, device=gpu) * 3
     rec = torch.zeros((), device=gpu)
     valid = torch.zeros((), device=gpu)
     sums = torch.zeros(2, dtype=torch.float64, device=gpu)

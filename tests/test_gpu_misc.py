@@ -83,6 +83,37 @@ def test_native_engine_step(gpu, tmp_path):
     assert torch.isfinite(eng.flat.flat).all().item()
 
 
+def test_early_bucket_step_matches_end_of_step(gpu, tmp_path, monkeypatch):
+    """Per-bucket SGD issued as soon as each bucket's gradients are final (one rank: the bucket
+    tracker without collectives, opt-in SDX_EARLY_STEP=1) == one whole-buffer SGD after backward, bit
+    for bit over two steps (elementwise update, identical gradients)."""
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    args = ["--batch_size", "32", "--synthetic", "--synthetic_size", "256", "--work_dir", str(tmp_path),
+            "--model", "resnet50", "--backend", "native"]
+    idx = torch.arange(32, device=gpu)
+    res, w0 = [], None
+    for early in ("0", "1"):
+        monkeypatch.setenv("SDX_EARLY_STEP", early)
+        eng = PretrainEngine(parse_pretrain(args, make_dirs=False))
+        assert (eng.reducer is not None) == (early == "1")
+        if early == "1":
+            assert len(eng.reducer.buckets) > 1 and not eng.reducer.enabled
+        if w0 is None:
+            w0 = eng.flat.flat.clone()
+        else:
+            eng.flat.flat.copy_(w0)
+        for it in range(2):
+            eng.train_step(idx, 1, it, 10)
+        torch.cuda.synchronize()
+        if early == "1":
+            assert sorted(eng.reducer.launch_log[:len(eng.reducer.buckets)]) == list(range(len(eng.reducer.buckets)))
+            assert eng.optimizer._applied == []
+        res.append((eng.flat.flat.clone(), eng.optimizer.buf.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("kind", ["fused", "emu"])
 def test_native_engine_step_emulated_syncbn(gpu, tmp_path, monkeypatch, kind):
     """The whole native training step (ResNet-50: stem, every block incl. the BN3 folds and the

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """From a rocprofv3 kernel trace of bench.py: wall time of the last training step
-(sgd_kernel end to sgd_kernel end), GPU-busy time (union of kernel intervals over all
+(wprep_kernel start to wprep_kernel start: the per-step weight conversion is the step's first
+kernel; the optimizer update runs per gradient bucket), GPU-busy time (union of kernel intervals over all
 streams) and idle gaps, plus the busiest kernels of that step.
 
 python tools/step_timeline.py <rocprof dir> [--dump FILE]
@@ -21,9 +22,9 @@ def main():
     for r in rows:
         r["Kernel_Name"] = r["Kernel_Name"].replace("(anonymous namespace)::", "")
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
-    a, b = idx[-2], idx[-1]
-    t0, t1 = int(rows[a]["End_Timestamp"]), int(rows[b]["End_Timestamp"])
+    idx = [i for i, r in enumerate(rows) if "wprep_kernel" in r["Kernel_Name"]]
+    a, b = idx[-2] - 1, idx[-1] - 1
+    t0, t1 = int(rows[a + 1]["Start_Timestamp"]), int(rows[b + 1]["Start_Timestamp"])
     busy, cur, gaps = 0, t0, []
     per = defaultdict(float)
     prev_name = rows[a]["Kernel_Name"]
