@@ -392,7 +392,16 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   }
 }
 
-int wgrad1x1_bn(const ConvGeom& g) { return g.C % 256 == 0 ? 256 : 128; }
+// SDX_W1_BN=128 forces the 128-column tile on every shape (co-residency experiments: the
+// non-pipelined 128x128 kernel holds 112 VGPRs, so an 8-wave main-stream block fits beside it)
+int wgrad1x1_bn(const ConvGeom& g) {
+  static const int force = [] {
+    const char* e = getenv("SDX_W1_BN");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 128) return 128;
+  return g.C % 256 == 0 ? 256 : 128;
+}
 
 bool w1_pipe_enabled(const ConvGeom& g) {
   static const bool on = [] {
