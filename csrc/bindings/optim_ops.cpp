@@ -11,7 +11,7 @@ void check_flat(const torch::Tensor& t, int64_t n, const char* name) {
 }
 
 void sgd_step(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor lr, double momentum, double wd,
-              double gscale, bool nesterov) {
+              double gscale, bool nesterov, int64_t max_blocks) {
   const int64_t n = p.numel();
   check_flat(p, n, "p");
   check_flat(g, n, "g");
@@ -20,7 +20,7 @@ void sgd_step(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor
   TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == at::kFloat && lr.numel() == 1, "lr must be a GPU float scalar");
   c10::DeviceGuard dg(p.device());
   check_hip(launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), n, lr.data_ptr<float>(),
-                       (float)momentum, (float)wd, (float)gscale, nesterov ? 1 : 0, cur_stream()),
+                       (float)momentum, (float)wd, (float)gscale, nesterov ? 1 : 0, cur_stream(), (int)max_blocks),
             "sgd_step");
 }
 
@@ -45,7 +45,9 @@ void lars_step(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tenso
 }  // namespace
 
 void register_optim(pybind11::module& m) {
-  m.def("sgd_step", &sgd_step, "fused flat-buffer SGD (momentum, wd, grad scale, device lr)");
+  m.def("sgd_step", &sgd_step, "fused flat-buffer SGD (momentum, wd, grad scale, device lr)", pybind11::arg("p"),
+        pybind11::arg("g"), pybind11::arg("buf"), pybind11::arg("lr"), pybind11::arg("momentum"), pybind11::arg("wd"),
+        pybind11::arg("gscale"), pybind11::arg("nesterov"), pybind11::arg("max_blocks") = 0);
   m.def("lars_step", &lars_step, "fused flat-buffer LARS");
 }
 

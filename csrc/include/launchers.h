@@ -238,7 +238,7 @@ hipError_t launch_gpu_augment(const uint8_t* data, const int64_t* idx, int B, in
 
 // ---- optimizers (optim.hip) -----------------------------------------------------
 hipError_t launch_sgd(float* p, const float* g, float* buf, long n, const float* lr, float momentum, float wd,
-                      float gscale, int nesterov, hipStream_t s);
+                      float gscale, int nesterov, hipStream_t s, int max_blocks = 0);
 hipError_t launch_lars(float* p, const float* g, float* buf, const long* seg_off, const int* adapt, int nseg, long n,
                        const float* lr, float momentum, float wd, float gscale, float eta, float* norms,
                        hipStream_t s);

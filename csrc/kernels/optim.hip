@@ -106,11 +106,14 @@ __global__ __launch_bounds__(256) void lars_kernel(float* __restrict__ p, const 
 }  // namespace
 
 hipError_t launch_sgd(float* p, const float* g, float* buf, long n, const float* lr, float momentum, float wd,
-                      float gscale, int nesterov, hipStream_t s) {
+                      float gscale, int nesterov, hipStream_t s, int max_blocks) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const long n4 = n / 4;
   long grid = (n4 + 255) / 256;
   if (grid > 4096) grid = 4096;
+  // a capped grid (grid-stride loop) trickles an early per-bucket update along beside the
+  // backward instead of taking every CU for a short burst
+  if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, s, p, g, buf, n4, lr, momentum, wd, gscale, nesterov);
   SDX_LAUNCH_CHECK();

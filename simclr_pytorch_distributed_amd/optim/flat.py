@@ -144,9 +144,11 @@ class FusedSGD(_FlatOptimizer):
     def apply_range(self, start: int, end: int):
         """Update the flat slice [start, end) now, on the current stream (the bucket reducer's
         early step: its gradients are final); :meth:`step` then skips it. Native path only."""
+        import os
         f = self.flat
+        blocks = int(os.environ.get("SDX_EARLY_STEP_BLOCKS", "0") or 0)
         _ext.require().sgd_step(f.flat[start:end], f.grad[start:end], self.buf[start:end], self.lr_t, self.momentum,
-                                self.weight_decay, self.grad_scale, self.nesterov)
+                                self.weight_decay, self.grad_scale, self.nesterov, blocks)
         self._applied.append((start, end))
 
     @torch.no_grad()
