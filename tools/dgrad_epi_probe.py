@@ -59,6 +59,20 @@ def main():
                         a.iters)
             print(f"{name} cfg {cfg:2d}: plain {tp:7.1f} us {mb / tp / 1e6:5.2f} TB/s | addend+stats {te:7.1f} us "
                   f"{me / te / 1e6:5.2f} TB/s | masked no-ya {tm:7.1f} us", flush=True)
+    # 3x3 stride-1 dgrads of the bottleneck's conv2 with the BN1-backward statistics epilogue
+    # (ya + ReLU bits, no addend), per stage
+    for name, N, H, C in [("l1c2", 512, 32, 64), ("l2c2", 512, 16, 128), ("l3c2", 512, 8, 256)]:
+        dy = torch.randn(N, H, H, C, device=dev).bfloat16()
+        wt = (torch.randn(C, 3, 3, C, device=dev) * 0.05).bfloat16()
+        ya = torch.randn(N, H, H, C, device=dev).bfloat16()
+        ma = torch.zeros(C, device=dev)
+        bits = torch.randint(0, 255, (N * H * H * C // 8,), device=dev, dtype=torch.uint8)
+        out = torch.empty_like(ya)
+        for cfg in cfgs:
+            tp = timeit(lambda: m.conv_dgrad(dy, wt, H, H, 1, 1, cfg, out), a.iters)
+            te = timeit(lambda: m.conv_dgrad_bnstat(dy, wt, H, H, 1, 1, cfg, out, None, None, ya, ma, mask_bits=bits),
+                        a.iters)
+            print(f"{name} cfg {cfg:2d}: plain {tp:7.1f} us | stats {te:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
