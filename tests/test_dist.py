@@ -111,6 +111,48 @@ def test_bucket_reducer_matches_allreduce(world):
     _run(_reducer_case, world)
 
 
+def _early_step_case(rank, world, d):
+    """early_step: each bucket's update is issued right after its all-reduce (bucket ranges
+    once each, covering every parameter) and the result equals reduce-then-update."""
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    from simclr_pytorch_distributed_amd.parallel.ddp import GradBucketReducer
+
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(64, 300), torch.nn.Linear(300, 500), torch.nn.Linear(500, 7))
+
+    lr = 0.1
+    m, ref = make(), make()
+    flat, fref = FlatParams(m), FlatParams(ref)
+    ranges = []
+
+    def early(start, end):
+        ranges.append((start, end))
+        with torch.no_grad():
+            flat.flat[start:end].sub_(lr * flat.grad[start:end])
+
+    red = GradBucketReducer(flat, bucket_mb=0.5, early_step=early)
+    assert red.active and red.enabled == (world > 1) and len(red.buckets) >= 2
+    x = torch.randn(5, 64) * (rank + 1)
+    for it in range(2):
+        ranges.clear()
+        flat.zero_grad()
+        m(x).square().sum().backward()
+        red.finish()
+        assert sorted(ranges) == [(b["start"], b["end"]) for b in red.buckets], ranges
+        fref.zero_grad()
+        ref(x).square().sum().backward()
+        g = fref.grad.clone()
+        dist.all_reduce(g)
+        fref.flat.sub_(lr * g)
+        assert torch.allclose(flat.flat, fref.flat, rtol=1e-5, atol=1e-5), it
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_early_step_reducer(world):
+    _run(_early_step_case, world)
+
+
 # --------------------------------------------------------------------------------------
 def _step_case(rank, world, d):
     from simclr_pytorch_distributed_amd.config import parse_pretrain
