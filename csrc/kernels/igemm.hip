@@ -63,6 +63,11 @@ constexpr int BK = 64;
 // profiles/nt_store_r2.txt); 0 restores write-back stores
 #define SDX_NT_STORE 1
 #endif
+#ifndef SDX_NT_STORE_DGRAD
+// the DGRAD outputs' store hint on its own (they are re-read at once by the BN-backward
+// passes, unlike most forward outputs); default: as SDX_NT_STORE
+#define SDX_NT_STORE_DGRAD SDX_NT_STORE
+#endif
 
 struct IgemmParams {
   ConvGeom g;
@@ -1204,7 +1209,8 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
           if (p.mask_out != nullptr) p.mask_out[o >> 3] = (uint8_t)relu_bits8(v);
         }
         // VAR 2 stores once, after the ReLU-backward mask below
-        if (VAR != 2 || !(MODE == MODE_DGRAD && bst)) st16<SDX_NT_STORE != 0>(out + o, v);
+        constexpr bool NTS = MODE == MODE_DGRAD ? SDX_NT_STORE_DGRAD != 0 : SDX_NT_STORE != 0;
+        if (VAR != 2 || !(MODE == MODE_DGRAD && bst)) st16<NTS>(out + o, v);
         if (MODE == MODE_DGRAD && bst) {
           // statistics of the stored (bf16-rounded) values, as bn_bwd_reduce would read them
           float d[8], ya[8];
@@ -1221,7 +1227,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
           // BN3 fold: dz = dout·[out > 0] of the previous block): the chunk is stored masked
           // (bf16 values already, so the repack is exact). Its own variant: the
           // BN-statistics kernels sit at the 128-VGPR occupancy step
-          if constexpr (VAR == 2) st16<SDX_NT_STORE != 0>(out + o, pack8(d));
+          if constexpr (VAR == 2) st16<SDX_NT_STORE_DGRAD != 0>(out + o, pack8(d));
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             bsum[0][q] += d[q];
