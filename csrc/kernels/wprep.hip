@@ -23,7 +23,10 @@ struct WSeg {
 
 // blockIdx.y = conv (segment); blockIdx.x = 64(k) x 64(c) tile at one filter tap rs.
 // Reads of the fp32 master and writes of Wk are coalesced along c; the transposed Wt tile
-// goes through LDS so its writes are coalesced along k.
+// goes through LDS so its writes are coalesced along k. Segments with C % 4 == 0 and no
+// channel padding (every conv but the stem, and the head's Linear layers) move 16-B float4
+// loads and 8-B bf16x4 stores per thread (a scalar fp32 load / 2-B store per element made
+// this a latency-bound 72 us pass per step).
 __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ master, uint16_t* __restrict__ out,
                                                     const WSeg* __restrict__ segs) {
   __shared__ uint16_t tile[64][66];
@@ -35,6 +38,44 @@ __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ ma
   const int rs = t % s.RS;
   const int kti = t / s.RS;
   const int k0 = kti * 64, c0 = cti * 64;
+  const bool vec = (s.C & 3) == 0 && s.Cp == s.C && (s.K & 3) == 0;
+  if (vec) {
+    // 16 threads per 64-channel row, 16 rows per pass, all 4 passes' loads in flight
+    const int cq = (threadIdx.x & 15) * 4, r0 = threadIdx.x >> 4;
+    const int c = c0 + cq;
+    float4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + r0 + 16 * i;
+      v[i] = (k < s.K && c < s.C) ? *reinterpret_cast<const float4*>(master + s.src + ((long)k * s.RS + rs) * s.C + c)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = r0 + 16 * i, k = k0 + kk;
+      const uint16_t b0 = f2bf(v[i].x), b1 = f2bf(v[i].y), b2 = f2bf(v[i].z), b3 = f2bf(v[i].w);
+      if (k < s.K && c < s.C)
+        *reinterpret_cast<uint2*>(out + s.dst_k + ((long)k * s.RS + rs) * s.Cp + c) =
+            make_uint2((uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16));
+      tile[kk][cq] = b0;
+      tile[kk][cq + 1] = b1;
+      tile[kk][cq + 2] = b2;
+      tile[kk][cq + 3] = b3;
+    }
+    if (s.dst_t < 0) return;
+    __syncthreads();
+    // transposed: 4 consecutive k of one input channel per thread (8-B stores along k)
+    const int kq = (threadIdx.x & 15) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cc = r0 + 16 * i, cw = c0 + cc, k = k0 + kq;
+      if (cw < s.C && k < s.K)
+        *reinterpret_cast<uint2*>(out + s.dst_t + ((long)cw * s.RS + rs) * s.K + k) =
+            make_uint2((uint32_t)tile[kq][cc] | ((uint32_t)tile[kq + 1][cc] << 16),
+                       (uint32_t)tile[kq + 2][cc] | ((uint32_t)tile[kq + 3][cc] << 16));
+    }
+    return;
+  }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int kk = ty; kk < 64; kk += 4) {
     const int k = k0 + kk, c = c0 + tx;

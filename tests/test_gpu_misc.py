@@ -324,3 +324,31 @@ def test_maxpool_index_backward(gpu, shape):
     xa = x.clone().requires_grad_(True)
     maxpool_nhwc(xa).backward(dy)
     assert torch.equal(xa.grad, d_new)
+
+
+def test_weight_cache_layouts_match_torch(gpu):
+    """One wprep launch (native, flat fp32 master) == the per-conv torch conversion of every
+    conv / head weight into the bf16 forward [K][R][S][Cp] and dgrad [C][R][S][K] layouts,
+    bit for bit (vectorised segments and the channel-padded stem)."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    torch.manual_seed(3)
+    m = SupConResNet("resnet50").to(gpu).to(memory_format=torch.channels_last)
+    flat = FlatParams(m)
+    with torch.no_grad():
+        flat.flat.normal_()
+    wc = ModelRunner(m, "native", master=flat.flat).weight_cache()
+    assert wc.native
+    wc.refresh()
+    for cv in wc.convs:
+        e = wc.entries[id(cv)]
+        w = cv.weight.detach()
+        w = w.view(w.shape[0], w.shape[1], 1, 1) if w.dim() == 2 else w
+        krsc = w.permute(0, 2, 3, 1).to(torch.bfloat16)
+        fk = wc.fwd(cv)
+        assert torch.equal(fk[..., :e["C"]], krsc)
+        if e["Cp"] > e["C"]:
+            assert not fk[..., e["C"]:].any()
+        if e["off_t"] >= 0:
+            assert torch.equal(wc.dgrad(cv), krsc.permute(3, 1, 2, 0))
