@@ -122,6 +122,9 @@ def pretrain_parser() -> argparse.ArgumentParser:
     g.add_argument("--optimizer", type=str, default="sgd", choices=["sgd", "lars"])
     g.add_argument("--grad_semantics", type=str, default="ref", choices=["ref", "exact"],
                    help="ref: DDP-mean of the global loss gradient (reference, SURVEY Q2); exact: W x that")
+    g.add_argument("--grad_compress", type=str, default="none", choices=["none", "bf16"],
+                   help="gradient bucket all-reduce payload: fp32 (reference DDP) or bf16 (half the "
+                        "xGMI bytes; sums rounded to bf16)")
     g.add_argument("--base_temperature", type=float, default=0.07)
     g.add_argument("--contrast_mode", type=str, default="all", choices=["all", "one"])
     g.add_argument("--resume", type=str, default="", help="resume model+optimizer+epoch+state from a ckpt")

@@ -147,7 +147,8 @@ class PretrainEngine:
         if (isinstance(self.optimizer, FusedSGD) and self.optimizer.native and not getattr(opt, "cuda_graph", False)
                 and os.environ.get("SDX_EARLY_STEP", "0") == "1"):
             early = self.optimizer.apply_range
-        self.reducer = GradBucketReducer(self.flat, early_step=early) if (world > 1 or early is not None) else None
+        self.reducer = (GradBucketReducer(self.flat, early_step=early, compress=getattr(opt, "grad_compress", "none"))
+                        if (world > 1 or early is not None) else None)
         self.optimizer.grad_scale = (1.0 / world) if opt.grad_semantics == "ref" else 1.0
         self.runner = ModelRunner(model, self.backend, opt.precision, self.sync_group, master=self.flat.flat)
         self.criterion = DistributedContrastiveLoss(opt.method, opt.temp, opt.base_temperature, opt.contrast_mode,

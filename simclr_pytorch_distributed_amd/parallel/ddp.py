@@ -26,7 +26,10 @@ reducer built on the flat gradient buffer of :class:`optim.flat.FlatParams`:
   the bucket's collective (or, with one rank, as soon as its gradients are final), so the
   elementwise update of the deeper layers runs while backward is still computing the
   shallow ones and only the last bucket's update is left after backward (the whole-buffer
-  SGD pass was ~90 us at the end of the ResNet-50 step). Used with one rank as well.
+  SGD pass was ~90 us at the end of the ResNet-50 step). Used with one rank as well;
+* ``compress='bf16'`` (``--grad_compress bf16``): each bucket is all-reduced as a bf16 copy
+  (half the bytes over the per-link-bound xGMI ring; the sum is rounded to bf16 — the
+  reference DDP reduces fp32, so this is opt-in) and written back into the fp32 buffer.
 """
 from __future__ import annotations
 
@@ -40,7 +43,7 @@ from . import comm
 
 class GradBucketReducer:
     def __init__(self, flat, bucket_mb: Optional[float] = None, group=None, enabled: Optional[bool] = None,
-                 broadcast_init: bool = True, early_step=None):
+                 broadcast_init: bool = True, early_step=None, compress: str = "none"):
         if bucket_mb is None:
             import os
             bucket_mb = float(os.environ.get("SDX_BUCKET_MB", "24"))
@@ -49,6 +52,9 @@ class GradBucketReducer:
         self.world = comm.world_size() if group is None else dist.get_world_size(group)
         self.enabled = (self.world > 1) if enabled is None else enabled   # all-reduce the buckets
         self.early_step = early_step
+        if compress not in ("none", "bf16"):
+            raise ValueError(f"compress must be 'none' or 'bf16', got {compress!r}")
+        self.compress = compress
         self.active = self.enabled or early_step is not None            # track bucket completion
         cap = int(bucket_mb * (1 << 20) / 4)
         # buckets in backward (= flat buffer) order
@@ -59,7 +65,7 @@ class GradBucketReducer:
             end = start + (flat.params[i].numel() + 4095) // 4096 * 4096
             if cur is None or (end - cur["start"]) > cap and cur["params"]:
                 cur = {"start": start, "end": end, "params": [], "ready": 0, "work": None, "launched": False,
-                       "idx": len(self.buckets)}
+                       "cbuf": None, "idx": len(self.buckets)}
                 self.buckets.append(cur)
             cur["params"].append(i)
             cur["end"] = end
@@ -114,6 +120,24 @@ class GradBucketReducer:
                 self._launch(b)
         return hook
 
+    def _reduce(self, b, view):
+        """Issue the bucket's collective (async); with bf16 compression on a bf16 copy."""
+        if self.compress == "bf16":
+            b["cbuf"] = view.to(torch.bfloat16)
+            b["work"] = dist.all_reduce(b["cbuf"], group=self.group, async_op=True)
+        else:
+            b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+
+    def _complete(self, b):
+        """Order the current stream after the bucket's collective (and copy a compressed sum
+        back into the fp32 buffer)."""
+        if b["work"] is not None:
+            b["work"].wait()
+            b["work"] = None
+        if b["cbuf"] is not None:
+            self.flat.grad[b["start"]:b["end"]].copy_(b["cbuf"])
+            b["cbuf"] = None
+
     def _launch(self, b):
         view = self.flat.grad[b["start"]:b["end"]]
         b["launched"] = True
@@ -129,20 +153,16 @@ class GradBucketReducer:
                 if streams.ENABLED:
                     self.comm_stream.wait_stream(streams.side(view.device))
                 if self.enabled:
-                    b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+                    self._reduce(b, view)
                 if self.early_step is not None:
-                    if b["work"] is not None:
-                        b["work"].wait()     # orders the comm stream after the collective
-                        b["work"] = None
+                    self._complete(b)        # orders the comm stream after the collective
                     self.early_step(b["start"], b["end"])
             self.launch_log.append(b["idx"])
         else:
             if self.enabled:
-                b["work"] = dist.all_reduce(view, group=self.group, async_op=True)
+                self._reduce(b, view)
             if self.early_step is not None:
-                if b["work"] is not None:
-                    b["work"].wait()
-                    b["work"] = None
+                self._complete(b)
                 self.early_step(b["start"], b["end"])
             self.launch_log.append(b["idx"])
 
@@ -171,9 +191,11 @@ class GradBucketReducer:
             if not b["launched"]:
                 self._launch(b)
         for b in self.buckets:
-            if b["work"] is not None:
-                b["work"].wait()
-            b["work"] = None
+            if self.comm_stream is not None and b["cbuf"] is not None:
+                with torch.cuda.stream(self.comm_stream):
+                    self._complete(b)
+            else:
+                self._complete(b)
             b["launched"] = False
             b["ready"] = 0
         self._seen = [False] * len(self._seen)

@@ -25,6 +25,8 @@ def main():
     argv = ["--model", name, "--backend", os.environ.get("SDX_TEST_BACKEND", "native"), "--dist_backend", "gloo", "--synthetic",
             "--synthetic_size", "64", "--learning_rate", "0.05", "--grad_semantics", "exact",
             "--work_dir", out_dir, "--batch_size", str(G), "--ngpu", str(world)]
+    if os.environ.get("SDX_TEST_GRAD_COMPRESS"):
+        argv += ["--grad_compress", os.environ["SDX_TEST_GRAD_COMPRESS"]]
     if world > 1:
         argv.append("--syncBN")
         # '' = rccl, which over the gloo process group means the Python collective path
@@ -52,7 +54,7 @@ def main():
     bn = eng.model.encoder.layer1[0].bn1
     torch.save({"flat": eng.flat.flat.detach().cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
                 "native_h": comm.native_small_comm(None), "loss": float(loss.detach()), "grad": grad.cpu(), "names": list(eng.flat.names),
-                "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"{name}_w{world}_r{rank}.pt"))
+                "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"{name}_w{world}{os.environ.get('SDX_TEST_GRAD_COMPRESS', '')}_r{rank}.pt"))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

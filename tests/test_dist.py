@@ -148,6 +148,37 @@ def _early_step_case(rank, world, d):
         assert torch.allclose(flat.flat, fref.flat, rtol=1e-5, atol=1e-5), it
 
 
+def _compress_case(rank, world, d):
+    """--grad_compress bf16: the buckets are reduced as bf16 copies and written back; the
+    result equals the fp32 all-reduce within bf16 rounding, and the reducer re-arms."""
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    from simclr_pytorch_distributed_amd.parallel.ddp import GradBucketReducer
+
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(64, 300), torch.nn.Linear(300, 500), torch.nn.Linear(500, 7))
+
+    m, ref = make(), make()
+    flat = FlatParams(m)
+    red = GradBucketReducer(flat, bucket_mb=0.5, compress="bf16")
+    x = torch.randn(5, 64) * (rank + 1)
+    for _ in range(2):
+        flat.zero_grad()
+        m(x).square().sum().backward()
+        red.finish()
+        assert all(b["cbuf"] is None and b["work"] is None for b in red.buckets)
+    ref.zero_grad()
+    ref(x).square().sum().backward()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        g = q.grad.clone()
+        dist.all_reduce(g)
+        assert torch.allclose(p.grad, g, rtol=2e-2, atol=2e-2 * g.abs().max().item()), (p.grad - g).abs().max()
+
+
+def test_bf16_compressed_reducer():
+    _run(_compress_case, 2)
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_early_step_reducer(world):
     _run(_early_step_case, world)

@@ -21,12 +21,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _launch(world, out, syncbn_comm="", model="resnet18"):
+def _launch(world, out, syncbn_comm="", model="resnet18", compress=""):
     # file-store rendezvous: no probed TCP port that another job on the box can take first
-    rdv = os.path.join(str(out), f"rdv_{model}_{world}_{syncbn_comm or 'pg'}")
+    rdv = os.path.join(str(out), f"rdv_{model}_{world}_{syncbn_comm or 'pg'}{compress}")
     procs = []
     for r in range(world):
         env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, SDX_TEST_MODEL=model, RANK=str(r), LOCAL_RANK="0",
+                   SDX_TEST_GRAD_COMPRESS=compress,
                    WORLD_SIZE=str(world), SDX_CONV_CFG="4",
                    MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD="file://" + rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
@@ -85,3 +86,20 @@ def test_two_rank_native_step_equals_single_rank(gpu, tmp_path, model, syncbn_co
     assert worst[0][0] < (4e-2 if model == "resnet50" else 2e-2), worst[:8]
     # global loss = sum of the ranks' row-owned losses
     assert abs(a["loss"] + b["loss"] - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3
+
+
+def test_two_rank_bf16_compressed_gradients(gpu, tmp_path):
+    """--grad_compress bf16 at W=2 (gloo on GPU tensors, buckets reduced as bf16 copies on the
+    comm stream and written back): replicas stay identical and every gradient matches the
+    W=1 step within bf16 rounding of the sums."""
+    _launch(1, tmp_path, "", "resnet18")
+    _launch(2, tmp_path, "", "resnet18", "bf16")
+    ref = torch.load(tmp_path / "resnet18_w1_r0.pt", weights_only=True)
+    a = torch.load(tmp_path / "resnet18_w2bf16_r0.pt", weights_only=True)
+    b = torch.load(tmp_path / "resnet18_w2bf16_r1.pt", weights_only=True)
+    assert torch.equal(a["grad"], b["grad"]) and torch.equal(a["flat"], b["flat"])
+    worst = max(float((a["grad"][o:o + k].double() - ref["grad"][o:o + k].double()).norm()
+                      / (ref["grad"][o:o + k].double().norm() + 1e-12))
+                for o, k in zip(a["offsets"], a["numels"]))
+    print(f"bf16-compressed W=2 vs W=1: worst parameter-gradient rel {worst:.3g}")
+    assert worst < 5e-2, worst
