@@ -15,7 +15,9 @@ def main():
     from simclr_pytorch_distributed_amd.config import parse_pretrain
     from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
     logging.disable(logging.INFO)
-    opt = parse_pretrain(["--batch_size", "256", "--synthetic", "--synthetic_size", "8192", "--backend", "native",
+    bs = os.environ.get("HP_BS", "256")          # HP_BS: images per step; HP_SYNC=1: idle queue
+    sync = os.environ.get("HP_SYNC", "0") == "1"  # (sync after each step: pure host cost)
+    opt = parse_pretrain(["--batch_size", bs, "--synthetic", "--synthetic_size", "8192", "--backend", "native",
                           "--work_dir", "/tmp/hp", "--temp", "0.5", "--cosine"], make_dirs=False)
     eng = PretrainEngine(opt)
     eng.model.train()
@@ -28,6 +30,8 @@ def main():
     pr.enable()
     for i in range(20):
         eng.train_step(idxs[5 + i], 1, 5 + i, len(idxs))
+        if sync:
+            torch.cuda.synchronize()
     pr.disable()
     torch.cuda.synchronize()
     st = pstats.Stats(pr)
