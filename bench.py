@@ -147,8 +147,11 @@ def main():
             graphed = eng.enable_cuda_graph(next_idx(0))
         except Exception as e:  # noqa: BLE001
             print(f"warning: hipGraph capture failed, eager fallback: {e!r}", file=sys.stderr)
+    first_loss = None
     for i in range(a.warmup):
-        eng.train_step(next_idx(i), 1, i % iters, iters)
+        st0 = eng.train_step(next_idx(i), 1, i % iters, iters)
+        if first_loss is None:
+            first_loss = st0["loss_local"]     # read after the timed region (no sync here)
     sync()
     # host cost of issuing one step into an idle queue (diagnostic, stderr)
     th = []
@@ -171,6 +174,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     loss = float(st["loss_local"].item())
+    loss0 = float(first_loss.item()) if first_loss is not None else None
     ms = dt / a.steps * 1e3
     value = global_batch * a.steps / dt
     d_in = {"resnet18": 512, "resnet34": 512}.get(a.model, 2048)
@@ -193,7 +197,12 @@ def main():
                        "backend": eng.backend, "syncbn_transport": eng.syncbn_transport, "hip_graph": graphed,
                        "views_per_sec": round(2 * value, 2),
                        "peak_hbm_gb": round(peak_gb, 2), "hbm_capacity_gb": 288,
-                       "last_loss_local": round(loss, 4)},
+                       # first warm-up step and last timed step: the run trains from random init
+                       # (44.5455 = every embedding identical, the collapse the reference recipe
+                       # lr 0.5 / no warm-up also reaches in fp32 torch on synthetic data in the
+                       # first ~20-60 steps: profiles/convergence_r1.txt)
+                       "first_loss_local": round(loss0, 4) if loss0 is not None else None,
+                       "last_loss_local": round(loss, 4), "loss_steps": a.warmup + 3 + a.steps},
         }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -57,7 +57,7 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
     const char* e = getenv("SDX_CONV_CFG");
     return e != nullptr ? atoi(e) : -1;
   }();
-  if (fill && pinned >= 0 && pinned <= 5) return pinned;
+  if (fill && pinned >= 0 && pinned <= 6) return pinned;
   const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
   const bool long_k = Kdim == 0 || Kdim > 256;
   const double pen_long[4] = {1.0, 1.04, 1.04, 1.35}, pen_short[4] = {1.0, 1.0, 1.0, 1.05};

@@ -46,6 +46,11 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
+#ifndef SDX_PP_WAIT_LATE
+// ping-pong loop (DEPTH 5): retire tile k+1's DMAs at the end of the compute segment (1) or of
+// the load segment (0)
+#define SDX_PP_WAIT_LATE 1
+#endif
 #ifndef SDX_ADD_PRE
 // DGRAD addend added to the fp32 accumulators before rounding when the launch asks for it
 // (GemmEpi::add_pre, BN3 fold): without it the fold's small mean-removal addend is swamped
@@ -85,7 +90,8 @@ struct IgemmParams {
   const float* in_scale;
   const float* in_shift;
   // diagnostic ablation (SDX_IGEMM_ABLATE bits, timing only — results are wrong):
-  // 1 skip LDS stores, 2 skip global loads, 4 skip MFMAs
+  // 1 skip LDS stores, 2 skip global loads / LDS-DMA, 4 skip MFMAs, 8 skip the fragment
+  // reads (ping-pong loop)
   int ablate;
   // log2(Q), log2(P*Q) when both are powers of two, else -1 (WGRAD pixel decode)
   int lq, lpq;
@@ -364,9 +370,9 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves");
   static_assert(T::A_CH >= 1 && T::B_CH >= 1, "tile too small for the thread count");
   constexpr int LDS_C = BM * (BN * 2 + 8);   // C-tile staging (epilogue)
-  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C) : (DEPTH == 4 ? 3 : 2) * T::STAGE;
+  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C) : (DEPTH >= 4 ? 3 : 2) * T::STAGE;
   static_assert(!ONE || DEPTH == 3, "single-stage variant is LDS-DMA only");
-  static_assert(DEPTH != 4 || MODE != MODE_WGRAD, "LDS-DMA ring is FWD/DGRAD only");
+  static_assert(DEPTH < 4 || MODE != MODE_WGRAD, "LDS-DMA ring is FWD/DGRAD only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const ConvGeom& g = p.g;
@@ -693,6 +699,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
 
   // LDS-DMA staging of one K-tile into LDS buffer `buf` (out-of-range chunks copy the zero page)
   auto issue_glds = [&](int k0, int buf) {
+    if (p.ablate & 2) return;
     unsigned char* sa = smem + buf * T::STAGE;
     unsigned char* sb = sa + T::A_BYTES;
     if (MODE == MODE_WGRAD) {
@@ -868,15 +875,12 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   };
 
   constexpr bool FRAG_PIN = SDX_FRAG_PIN;
-  auto compute = [&](int buf) {
-    if (p.ablate & 4) return;
+  // all fragments of both 32-deep k-steps of a K-tile (distinct registers, so the MFMAs of
+  // step 0 overlap the LDS latency of step 1 and no lgkmcnt(0) drain sits between MFMA
+  // groups: the compiler otherwise recycles two A-fragment registers and stalls on each refill)
+  auto read_frags = [&](int buf, bf16x8 (&af)[2][TM], bf16x8 (&bfr)[2][TN]) {
     const unsigned char* sa = smem + buf * T::STAGE;
     const unsigned char* sb = sa + T::A_BYTES;
-    // all fragments of both 32-deep k-steps are requested up front (distinct registers),
-    // so the MFMAs of step 0 overlap the LDS latency of step 1 and no lgkmcnt(0) drain
-    // sits between MFMA groups (the compiler otherwise recycles two A-fragment registers
-    // and stalls on each refill)
-    bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -890,7 +894,8 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         else af[u][i] = frag_kout(sa, wm * WTM + 16 * i, u, std::integral_constant<int, BM>{});
       }
     }
-    if (FRAG_PIN) __builtin_amdgcn_sched_barrier(0);   // keep all fragment reads ahead of the MFMAs
+  };
+  auto mfma_tile = [&](const bf16x8 (&af)[2][TM], const bf16x8 (&bfr)[2][TN]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -900,15 +905,82 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
           // D = Bᵀ·Aᵀ: accumulator column = output row (lane c), rows = output columns (4h + r)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[u][j], af[u][i], acc[i][j], 0, 0, 0);
   };
+  auto compute = [&](int buf) {
+    if (p.ablate & 4) return;
+    bf16x8 af[2][TM], bfr[2][TN];
+    read_frags(buf, af, bfr);
+    if (FRAG_PIN) __builtin_amdgcn_sched_barrier(0);   // keep all fragment reads ahead of the MFMAs
+    mfma_tile(af, bfr);
+  };
 
   // 8-wave blocks: the second-dispatched half loses VALU/issue arbitration to the older half
   // on every segment; one static priority raise for it (no per-cluster flips). SDX_PRIO_HALF
-  if (SDX_PRIO_HALF && NT == 512 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  // (not in the ping-pong loop, whose halves take turns by construction)
+  if (SDX_PRIO_HALF && NT == 512 && DEPTH != 5 && __builtin_amdgcn_readfirstlane(tid) >= 256)
+    __builtin_amdgcn_s_setprio(1);
   // K loop: two LDS buffers, one barrier per K-tile. DEPTH 1: the loads of tile k+1 are in
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
   // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
   // issued a whole K-tile earlier (load latency covered by two tiles of MFMA work).
-  if (DEPTH == 4) {
+  if constexpr (DEPTH == 5) {
+    // Ping-pong over a 3-buffer LDS-DMA ring (8-wave blocks, one per CU). Every wave
+    // alternates a LOAD segment (the fragment ds_reads of tile k into registers, then its
+    // share of tile k+2's LDS-DMA) and a COMPUTE segment (tile k's MFMAs on those
+    // registers), one raw barrier between segments. Waves 4-7 run one segment behind waves
+    // 0-3, so on every SIMD one wave's MFMAs overlap its partner's LDS reads and DMA issue
+    // instead of all 8 waves contending for the LDS in lockstep and then for the matrix
+    // pipe (cdna_hip_programming.md §5 8-phase template, T3/T4: counted vmcnt, raw
+    // s_barrier, never a vmcnt(0) drain in the loop).
+    // Ordering (segment s = one barrier interval; group 0 loads tile k in s = 2k, group 1
+    // in 2k+1): RAW — a wave retires its own DMAs of tile k+1 with the counted vmcnt at
+    // the end of its load segment k, before a barrier every reader of tile k+1 has passed
+    // (group 0 reads it in 2k+2, group 1 in 2k+3). WAR — tile k+2 overwrites the buffer of
+    // tile k-1, which group 1 last read in segment 2k-1 and retired (lgkmcnt(0)) before the
+    // barrier ending it; group 0's DMA issue is in segment 2k. Past-the-end tiles are not
+    // issued, so the last two load segments drain the queue (vmcnt(0)).
+    static_assert(NT == 512, "ping-pong needs two 4-wave groups");
+    constexpr int NL = T::A_CH + T::B_CH;   // LDS-DMA instructions per wave per tile
+    const bool late = wvu >= 4;
+    issue_glds(k_begin, 0);
+    issue_glds(k_begin + BK, 1);
+    vm_wait<NL>();
+    lds_barrier();
+    if (late) lds_barrier();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      bf16x8 af[2][TM], bfr[2][TN];
+      if (p.ablate & 8) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[u][i] = bf16x8{};
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bfr[u][j] = bf16x8{};
+        }
+      } else {
+        read_frags(buf, af, bfr);
+      }
+      const bool more = kt + 2 < nk;
+      if (more) issue_glds(k_begin + (kt + 2) * BK, buf == 0 ? 2 : buf - 1);
+      if (SDX_PP_WAIT_LATE == 0) {
+        if (more) vm_wait<NL>(); else vm_wait<0>();
+      }
+      lds_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      if (!(p.ablate & 4)) mfma_tile(af, bfr);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // the wait for this wave's DMAs of tile k+1 sits behind the MFMAs: tile k+1 is read
+      // only in the next load segment, so its transfer gets three segments of cover
+      if (SDX_PP_WAIT_LATE != 0) {
+        if (more) vm_wait<NL>(); else vm_wait<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      buf = buf == 2 ? 0 : buf + 1;
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+  } else if (DEPTH == 4) {
     // 3-buffer LDS-DMA ring: tile k+2's DMA is issued while tile k computes. The counted
     // vmcnt before each raw barrier retires only tile k; tile k+1 stays in flight across
     // it (a __syncthreads() would drain every DMA: its fence waits vmcnt(0)). The buffer
@@ -1402,6 +1474,15 @@ int igemm_ring() {
   return v;
 }
 
+// ping-pong main loop of the 8-wave 256x128 / 128x256 tiles (SDX_IGEMM_PP=0: DEPTH 3 instead)
+int igemm_pp() {
+  static const int v = [] {
+    const char* e = getenv("SDX_IGEMM_PP");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int igemm_worder() {
   static const int v = [] {
     const char* e = getenv("SDX_WGRAD_ORDER");
@@ -1418,67 +1499,50 @@ int igemm_one() {
   return v;
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
-hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR>
+hipError_t launch_v(bool one, int grid, const IgemmParams& p, hipStream_t s) {
   const dim3 g(grid), b(64 * WM * WN);
-  if (MODE == MODE_FWD && p.bn_sc != nullptr) {
-    // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
-    if constexpr (MODE == MODE_FWD && DEPTH == 3) {
-      if (p.Kdim <= BK && igemm_one())
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, true>), g, b, 0, s, p);
-      else
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, false>), g, b, 0, s, p);
+  if constexpr (DEPTH == 3) {
+    if (one) {
+      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, VAR, true>), g, b, 0, s, p);
       SDX_LAUNCH_CHECK();
       return hipSuccess;
     }
+  }
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, VAR, false>), g, b, 0, s, p);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
+hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
+  // LDS-DMA main loops (DEPTH 3: two buffers; 5: ping-pong ring) carry every epilogue
+  // variant; the single-stage (ONE) form is DEPTH 3 at one K-tile
+  constexpr bool GLK = (DEPTH == 3 || DEPTH == 5) && MODE != MODE_WGRAD;
+  const bool one = DEPTH == 3 && p.Kdim <= BK && igemm_one();
+  if (MODE == MODE_FWD && p.bn_sc != nullptr) {
+    // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
+    if constexpr (MODE == MODE_FWD && GLK) return launch_v<MODE, BM, BN, WM, WN, DEPTH, 2>(one, grid, p, s);
     return hipErrorInvalidValue;
   }
   if (bs && p.bs.store_masked) {
     // masked-store statistics variant (projection head, BN3 fold): LDS-DMA tiles only
-    if constexpr (MODE == MODE_DGRAD && DEPTH == 3) {
-      if (p.Kdim <= BK && igemm_one())
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, true>), g, b, 0, s, p);
-      else
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 2, false>), g, b, 0, s, p);
-      SDX_LAUNCH_CHECK();
-      return hipSuccess;
-    }
+    if constexpr (MODE == MODE_DGRAD && GLK) return launch_v<MODE, BM, BN, WM, WN, DEPTH, 2>(one, grid, p, s);
     return hipErrorInvalidValue;
   }
   if (p.sf.cnt != nullptr) {
     // in-kernel statistics reduction: LDS-DMA variants only (launch_cfg routes here)
-    if constexpr (DEPTH == 3 && MODE != MODE_WGRAD) {
+    if constexpr (GLK) {
       constexpr int V = MODE == MODE_DGRAD ? 3 : 1;
       if (MODE == MODE_DGRAD && !bs) return hipErrorInvalidValue;
-      if (p.Kdim <= BK && igemm_one())
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, V, true>), g, b, 0, s, p);
-      else
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, V, false>), g, b, 0, s, p);
-      SDX_LAUNCH_CHECK();
-      return hipSuccess;
+      return launch_v<MODE, BM, BN, WM, WN, DEPTH, V>(one, grid, p, s);
     }
     return hipErrorInvalidValue;
   }
-  if constexpr (DEPTH == 3 && MODE != MODE_WGRAD) {
-    if (p.Kdim <= BK && igemm_one()) {
-      if (MODE == MODE_DGRAD && bs)
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, MODE == MODE_DGRAD ? 1 : 0, true>), g, b, 0, s, p);
-      else
-        hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 0, true>), g, b, 0, s, p);
-      SDX_LAUNCH_CHECK();
-      return hipSuccess;
-    }
-  }
   if constexpr (MODE == MODE_DGRAD) {
-    if (bs) {
-      hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 1, false>), g, b, 0, s, p);
-      SDX_LAUNCH_CHECK();
-      return hipSuccess;
-    }
+    if (bs) return launch_v<MODE, BM, BN, WM, WN, DEPTH, 1>(one, grid, p, s);
   }
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, DEPTH, 0, false>), g, b, 0, s, p);
-  SDX_LAUNCH_CHECK();
-  return hipSuccess;
+  return launch_v<MODE, BM, BN, WM, WN, DEPTH, 0>(one, grid, p, s);
 }
 
 // WGRAD launch of variant VAR (bit 0: 1x1 fast path, bit 1: BN prologue) at the depth
@@ -1520,11 +1584,20 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   {
     // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
     // (SDX_IGEMM_GLDS=2 enables it there too)
+    // ping-pong main loop: the 8-wave 256x128 / 128x256 tiles at more than two K-tiles
+    constexpr bool kPP = WM * WN == 8 && BM * BN == 256 * 128;
+    const bool pp = kPP && igemm_pp() && p.Kdim > 2 * BK && p.in_scale == nullptr;
     if (p.sf.cnt != nullptr) {
       if (p.in_scale != nullptr) return hipErrorInvalidValue;
+      if constexpr (kPP) {
+        if (pp) return launch_k<MODE, BM, BN, WM, WN, 5>(bs, grid, p, s);
+      }
       return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
     }
     if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
+      if constexpr (kPP) {
+        if (pp) return launch_k<MODE, BM, BN, WM, WN, 5>(bs, grid, p, s);
+      }
       if constexpr (MODE != MODE_WGRAD) {
         if (igemm_ring() && p.Kdim > 2 * BK) return launch_k<MODE, BM, BN, WM, WN, 4>(bs, grid, p, s);
       }
@@ -1544,7 +1617,8 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
 
 // tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
 // 4 128x128 with 8 waves (2x4 of 64x32: twice the waves per SIMD for latency hiding),
-// 5 256x128 with 8 waves (4x2 of 64x64, 96 KiB LDS: one block per CU)
+// 5 256x128 with 8 waves (4x2 of 64x64, one block per CU), 6 128x256 with 8 waves (2x4 of
+// 64x64); both run the ping-pong main loop (DEPTH 5, 144 KiB LDS ring) at K > 128
 template <int MODE>
 hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
   switch (cfg) {
@@ -1554,6 +1628,7 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
     case 3: return launch_cfg<MODE, 64, 64, 2, 2>(p, s);
     case 4: return launch_cfg<MODE, 128, 128, 2, 4>(p, s);
     case 5: return launch_cfg<MODE, 256, 128, 4, 2>(p, s);
+    case 6: return launch_cfg<MODE, 128, 256, 2, 4>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1561,11 +1636,11 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
 }  // namespace
 
 int igemm_tile_m(int cfg) {
-  static const int m[6] = {128, 256, 64, 64, 128, 256};
+  static const int m[7] = {128, 256, 64, 64, 128, 256, 128};
   return m[cfg];
 }
 int igemm_tile_n(int cfg) {
-  static const int n[6] = {128, 64, 256, 64, 128, 128};
+  static const int n[7] = {128, 64, 256, 64, 128, 128, 256};
   return n[cfg];
 }
 

@@ -129,6 +129,38 @@ def ragged_side_cap(size: int, min_scale: float = 0.2, min_ratio: float = 3 / 4)
     return int(math.ceil(size / math.sqrt(min_scale * min_ratio)))
 
 
+def fit_ragged_budget(sizes: np.ndarray, budget: int, min_side: int = 1):
+    """Shrink a ragged store's per-image (h, w) so its bytes fit ``budget``: every shorter
+    side above a common cap is scaled down to it, aspect ratio kept (RandomResizedCrop then
+    still samples its boxes from the native geometry, unlike a squashed square store). The
+    cap starts at cap·sqrt(budget/total) and is lowered until the store fits; it never goes
+    below ``min_side`` (the crop output size) — a folder that does not fit even then raises
+    instead of silently degrading the augmentation. Returns (sizes, cap or None)."""
+    import math
+    sizes = np.asarray(sizes, dtype=np.int32).reshape(-1, 2)
+
+    def total_of(sz):
+        return int((sz[:, 0].astype(np.int64) * sz[:, 1] * 3).sum())
+
+    total = total_of(sizes)
+    if total <= budget:
+        return sizes, None
+    short = sizes.min(axis=1).astype(np.float64)
+    cap = int(math.floor(short.max() * math.sqrt(budget / total)))
+    while True:
+        cap = max(int(min_side), cap)
+        f = np.minimum(1.0, cap / np.maximum(short, 1.0))
+        out = np.stack([np.maximum(1, np.round(sizes[:, 0] * f)), np.maximum(1, np.round(sizes[:, 1] * f))],
+                       axis=1).astype(np.int32)
+        if total_of(out) <= budget:
+            return out, cap
+        if cap <= min_side:
+            raise RuntimeError(
+                f"image store needs {total_of(out) / 2**30:.1f} GiB even with shorter sides capped at "
+                f"{cap} px (> budget {budget / 2**30:.1f} GiB): raise SDX_DATA_BUDGET_GB")
+        cap = int(cap * 0.97)
+
+
 DATA_BUDGET_BYTES = int(float(os.environ.get("SDX_DATA_BUDGET_GB", "64")) * (1 << 30))
 
 
@@ -142,8 +174,9 @@ def load_image_folder(root: str, size: Optional[int] = None, workers: int = 1, m
     The shorter side is capped at ``max_side`` (aspect kept; see :func:`ragged_side_cap`),
     the sizes are read from the headers first and the flat store is preallocated and
     filled in place (no second copy). If the store would exceed ``budget_bytes`` (default
-    ``SDX_DATA_BUDGET_GB``, 64 GiB: it lives in HBM next to training) the dense
-    ``dense_size``-resized store is built instead. ``size=s``: resized to s x s into a
+    ``SDX_DATA_BUDGET_GB``, 64 GiB: it lives in HBM next to training) the shorter-side cap
+    is lowered until it fits (:func:`fit_ragged_budget`; aspect ratios kept, never below
+    ``dense_size``), or a RuntimeError asks for a larger budget. ``size=s``: resized to s x s into a
     dense [N, s, s, 3] array. Decoding runs on ``workers`` threads (``--num_workers``; PIL
     releases the GIL while decoding).
     """
@@ -196,14 +229,13 @@ def load_image_folder(root: str, size: Optional[int] = None, workers: int = 1, m
 
     with ThreadPoolExecutor(max_workers=nw) as ex:
         sizes = np.asarray(list(ex.map(header, files)), dtype=np.int32).reshape(-1, 2)
+    budget = DATA_BUDGET_BYTES if budget_bytes is None else int(budget_bytes)
+    sizes, cap = fit_ragged_budget(sizes, budget, min_side=dense_size or 1)
+    if cap is not None:
+        logging.warning(f"native-resolution store of {root!r} exceeds the {budget / 2**30:.1f} GiB budget: "
+                        f"shorter sides capped at {cap} px (aspect kept; raise SDX_DATA_BUDGET_GB to keep more)")
     nbytes = sizes[:, 0].astype(np.int64) * sizes[:, 1] * 3
     total = int(nbytes.sum())
-    budget = DATA_BUDGET_BYTES if budget_bytes is None else int(budget_bytes)
-    if total > budget:
-        s = dense_size or (max_side or 256)
-        logging.warning(f"native-resolution store of {root!r} needs {total / 2**30:.1f} GiB > budget "
-                        f"{budget / 2**30:.1f} GiB: using a dense {s}x{s} store")
-        return dense(s)
     offsets = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.int64)
     flat = np.empty(total, dtype=np.uint8)
 

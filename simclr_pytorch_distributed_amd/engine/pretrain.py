@@ -188,14 +188,14 @@ class PretrainEngine:
     def _setup_syncbn_comm(self, opt, dev):
         """SyncBN statistics transport for the native backend.
 
-        ``--syncbn_comm auto`` (default) / ``xgmi``: the one-shot IPC arena, whose FUSED
+        ``--syncbn_comm auto`` / ``xgmi`` (opt-in): the one-shot IPC arena, whose FUSED
         path reduces, exchanges and finalizes every BN's statistics in one launch
         (parallel/xgmi.py); ``auto`` uses it whenever all ranks are peers on one node and
-        falls back to RCCL otherwise. ``rccl``: a dedicated RCCL communicator. Either is
+        falls back to RCCL otherwise. ``rccl`` (default): a dedicated RCCL communicator. Either is
         registered as a native handle, so the C++ block executor exchanges each BN's sums
         itself on the compute stream. gloo (CPU tests, shared-GPU tests) keeps the Python
         collective path."""
-        want = getattr(opt, "syncbn_comm", "auto")
+        want = getattr(opt, "syncbn_comm", "rccl")
         if dev.type != "cuda":
             return
         timeout = float(getattr(opt, "comm_timeout", 600.0))

@@ -109,6 +109,10 @@ class _FlatOptimizer:
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
+        # a new step starts: slices an abandoned step updated early must not be skipped by
+        # the next step()
+        if hasattr(self, "_applied"):
+            self._applied = []
 
     def state_dict(self) -> Dict:
         """torch.optim.SGD-format state dict (per-parameter momentum_buffer)."""
@@ -139,16 +143,16 @@ class FusedSGD(_FlatOptimizer):
         self.nesterov = nesterov
         self.native = backend != "torch" and flat.flat.is_cuda and _ext.available()
         self._applied = []      # [start, end) slices updated early this step (apply_range)
+        import os
+        self._early_blocks = int(os.environ.get("SDX_EARLY_STEP_BLOCKS", "0") or 0)
 
     @torch.no_grad()
     def apply_range(self, start: int, end: int):
         """Update the flat slice [start, end) now, on the current stream (the bucket reducer's
         early step: its gradients are final); :meth:`step` then skips it. Native path only."""
-        import os
         f = self.flat
-        blocks = int(os.environ.get("SDX_EARLY_STEP_BLOCKS", "0") or 0)
         _ext.require().sgd_step(f.flat[start:end], f.grad[start:end], self.buf[start:end], self.lr_t, self.momentum,
-                                self.weight_decay, self.grad_scale, self.nesterov, blocks)
+                                self.weight_decay, self.grad_scale, self.nesterov, self._early_blocks)
         self._applied.append((start, end))
 
     @torch.no_grad()

@@ -35,6 +35,9 @@ def test_bench_two_ranks_json_contract(tmp_path):
     assert d["scaling"] == "weak" and d["higher_is_better"] is True
     c = d["config"]
     assert c["global_batch"] == 8 and c["per_gpu_batch"] == 4 and c["parallelism"] == "dp2+syncbn"
+    # the timed run is a training run: first (warm-up) and last (timed) step losses are reported
+    assert isinstance(c["first_loss_local"], float) and isinstance(c["last_loss_local"], float)
+    assert c["loss_steps"] == 1 + 3 + 2
     # value = whole-job images/s = global batch x steps / time
     assert abs(d["value"] - 8 * 1e3 / d["ms_per_step"]) / d["value"] < 0.01
 

@@ -35,8 +35,10 @@ def test_image_folder_native_and_resized(tmp_path):
 
 
 def test_image_folder_side_cap_and_budget(tmp_path):
-    """The ragged store caps the shorter side at ragged_side_cap(size) (aspect kept) and
-    falls back to the dense resized store when it would exceed the byte budget."""
+    """The ragged store caps the shorter side at ragged_side_cap(size) (aspect kept); over
+    the byte budget it lowers that cap (still ragged, aspect ratios kept: RandomResizedCrop
+    keeps sampling the native geometry) and raises when even a cap at the crop size does not
+    fit (no silent squashed square store)."""
     from simclr_pytorch_distributed_amd.data.datasets import load_image_folder, ragged_side_cap
     assert ragged_side_cap(32) == 83 and ragged_side_cap(224) == 579
     _folder(tmp_path, [(120, 60), (40, 200), (30, 30)])
@@ -44,8 +46,14 @@ def test_image_folder_side_cap_and_budget(tmp_path):
     hw = sorted(tuple(int(v) for v in s) for s in ds.sizes)
     assert hw == sorted([(100, 50), (40, 200), (30, 30)])
     assert ds.images.size == sum(h * w * 3 for h, w in hw)
-    small = load_image_folder(str(tmp_path), None, 2, max_side=50, budget_bytes=1000, dense_size=16)
-    assert not small.ragged and small.images.shape == (3, 16, 16, 3)
+    small = load_image_folder(str(tmp_path), None, 2, max_side=50, budget_bytes=20000, dense_size=16)
+    assert small.ragged and small.images.size <= 20000
+    hw2 = sorted(tuple(int(v) for v in s) for s in small.sizes)
+    assert hw2 == sorted([(56, 28), (28, 140), (28, 28)])       # shorter sides capped at 28
+    for (h, w), (h2, w2) in zip(hw, hw2):
+        assert abs(h / w - h2 / w2) < 0.05 * (h / w)
+    with pytest.raises(RuntimeError, match="SDX_DATA_BUDGET_GB"):
+        load_image_folder(str(tmp_path), None, 2, max_side=50, budget_bytes=1000, dense_size=16)
 
 
 def test_ragged_reference_augment_matches_dense():

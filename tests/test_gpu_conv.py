@@ -14,6 +14,8 @@ SHAPES = [
     (4, 8, 8, 256, 512, 1, 2, 0),    # strided 1x1 shortcut
     (8, 8, 8, 8, 64, 3, 1, 1),       # stem (C padded to 8)
     (2, 4, 4, 512, 512, 3, 1, 1),    # layer4 shape
+    (8, 16, 16, 128, 256, 3, 1, 1),  # several 256-row tiles, 18 K-tiles (ping-pong ring wraps)
+    (4, 16, 16, 192, 320, 1, 1, 0),  # 3 K-tiles (shortest ping-pong), ragged N vs 128/256
 ]
 
 
@@ -29,7 +31,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 def test_conv_fwd(gpu, shape, cfg):
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
@@ -49,7 +51,7 @@ def test_conv_fwd(gpu, shape, cfg):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 def test_conv_dgrad(gpu, shape, cfg):
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
@@ -218,8 +220,8 @@ def test_dgrad_masked_addend(gpu):
     assert _rel(out, exp) < 1e-2
 
 
-@pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[3] & (s[3] - 1) == 0])   # bn backward: power-of-two C
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("mask", ["none", "bits", "affine"])
 def test_dgrad_bn_stats_epilogue(gpu, shape, cfg, mask):
     """conv_dgrad_bnstat: dx identical to conv_dgrad; its slab sums to Σd·m, Σd·m·(y−μ)
