@@ -46,11 +46,6 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
-#ifndef SDX_PP_WAIT_LATE
-// ping-pong loop (DEPTH 5): retire tile k+1's DMAs at the end of the compute segment (1) or of
-// the load segment (0)
-#define SDX_PP_WAIT_LATE 1
-#endif
 #ifndef SDX_ADD_PRE
 // DGRAD addend added to the fp32 accumulators before rounding when the launch asks for it
 // (GemmEpi::add_pre, BN3 fold): without it the fold's small mean-removal addend is swamped
@@ -962,20 +957,16 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       }
       const bool more = kt + 2 < nk;
       if (more) issue_glds(k_begin + (kt + 2) * BK, buf == 0 ? 2 : buf - 1);
-      if (SDX_PP_WAIT_LATE == 0) {
-        if (more) vm_wait<NL>(); else vm_wait<0>();
-      }
+      // retire this wave's DMAs of tile k+1 before the barrier: group 0 reads that tile in
+      // the very next segment (a wait placed after the MFMAs would be too late for group 1's
+      // share, which group 0 reads during group 1's compute segment)
+      if (more) vm_wait<NL>(); else vm_wait<0>();
       lds_barrier();
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
       if (!(p.ablate & 4)) mfma_tile(af, bfr);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      // the wait for this wave's DMAs of tile k+1 sits behind the MFMAs: tile k+1 is read
-      // only in the next load segment, so its transfer gets three segments of cover
-      if (SDX_PP_WAIT_LATE != 0) {
-        if (more) vm_wait<NL>(); else vm_wait<0>();
-      }
       __builtin_amdgcn_s_barrier();
       buf = buf == 2 ? 0 : buf + 1;
     }
