@@ -57,7 +57,7 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
     const char* e = getenv("SDX_CONV_CFG");
     return e != nullptr ? atoi(e) : -1;
   }();
-  if (fill && pinned >= 0 && pinned <= 6) return pinned;
+  if (fill && pinned >= 0 && pinned <= 8) return pinned;
   const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
   const bool long_k = Kdim == 0 || Kdim > 256;
   const double pen_long[4] = {1.0, 1.04, 1.04, 1.35}, pen_short[4] = {1.0, 1.0, 1.0, 1.05};
@@ -1597,6 +1597,13 @@ void register_conv_bn(pybind11::module& m) {
         "in-kernel BN-statistics reduction of the block executor (bits: 1 forward, 2 backward); returns the "
         "previous bits",
         pybind11::arg("bits"));
+  m.def("igemm_trace", [] {
+    const int n = 2 * igemm_trace_slots();
+    auto t = torch::empty({n}, torch::TensorOptions().dtype(at::kLong));
+    check_hip(igemm_trace_copy(reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>()), cur_stream()),
+              "igemm_trace");
+    return t.view({2, n / 2});
+  }, "diagnostic conv main-loop timeline of the last traced launch (SDX_IGEMM_TRACE=1)");
   m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16) + BN stat slab [+ BN+ReLU prologue]",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("want_stats"), pybind11::arg("cfg") = -1, pybind11::arg("in_scale") = pybind11::none(),

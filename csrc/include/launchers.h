@@ -87,6 +87,9 @@ struct GemmEpi {
 };
 bool conv_fwd_bnapply_supported();
 int igemm_tile_m(int cfg);
+// diagnostic main-loop timeline (SDX_IGEMM_TRACE=1): block 0, waves 0 and 4, s_memtime stamps
+int igemm_trace_slots();
+hipError_t igemm_trace_copy(unsigned long long* host, hipStream_t s);
 int igemm_tile_n(int cfg);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
 struct StatFuse;

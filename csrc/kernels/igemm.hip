@@ -46,6 +46,9 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
+#ifndef SDX_W1_SGB
+#define SDX_W1_SGB 1   // DEPTH 6: sched_group_barrier interleave of the second half
+#endif
 #ifndef SDX_ADD_PRE
 // DGRAD addend added to the fp32 accumulators before rounding when the launch asks for it
 // (GemmEpi::add_pre, BN3 fold): without it the fold's small mean-removal addend is swamped
@@ -68,6 +71,14 @@ constexpr int BK = 64;
 // passes, unlike most forward outputs); default: as SDX_NT_STORE
 #define SDX_NT_STORE_DGRAD SDX_NT_STORE
 #endif
+
+// Diagnostic main-loop timeline (SDX_IGEMM_TRACE=1, tools/igemm_trace.py): lane 0 of waves 0
+// and 4 of block 0 store s_memtime stamps (vector stores) at fixed events; row w of
+// [2][kTraceSlots]: 0 kernel start, 1 loop start, 2 + 3·kt + {0: fragment reads + DMA issued,
+// 1: after the load barrier, 2: MFMAs issued}, kTraceSlots-4 loop end, -3 epilogue staged,
+// -2 end, -1 s_memrealtime at the end (100 MHz) with slot -5 the one at the start.
+constexpr int kTraceSlots = 512;
+__device__ unsigned long long g_igemm_trace[2 * kTraceSlots];
 
 struct IgemmParams {
   ConvGeom g;
@@ -102,6 +113,7 @@ struct IgemmParams {
   const float* bias;
   int relu, out_f32;
   int add_pre;   // GemmEpi::add_pre
+  int trace;     // g_igemm_trace stamps (diagnostic)
   // FWD VAR 2 (GemmEpi::bn_scale): the block-output BatchNorm applied in the epilogue —
   // out = relu(bf16(y)·bn_sc + bn_sh + addend), its ReLU bits to mask_out (1 bit per element)
   const float* bn_sc;
@@ -159,6 +171,17 @@ __device__ __forceinline__ gptr16 opaque_zero() {
   gptr16 z = (gptr16)g_zero16;
   asm volatile("" : "+s"(z));
   return z;
+}
+
+// One 16-B LDS-DMA (global_load_lds_dwordx4). The source address goes through an empty asm
+// that pins it in a VGPR pair: hipcc otherwise splits "ok ? row address : zero page" into
+// two exec-masked branches, each with its own glds (the zero page through the scalar-base
+// form), which doubles the DMA instructions and serialises them behind SALU exec juggling
+// (seen in the .s of every LDS-DMA variant; issue cost ~1000 cycles per K-tile per wave).
+__device__ __forceinline__ void glds16(gptr16 src, void* lds) {
+  asm volatile("" : "+v"(src));
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
 // relu(x·s + t) on 8 packed bf16 channels (fp32 math, one rounding: same as bn_apply)
@@ -351,6 +374,8 @@ __device__ __forceinline__ void stat_fuse_tail(const StatFuse& f, const float* s
 // occupancy of their plain statistics variant (the tail would otherwise cost one wave)
 template <int MODE, int BM, int BN, int WM, int WN, int VAR>
 constexpr int igemm_min_waves() {
+  // 4-wave blocks of 64x128 / 128x64 wave tiles (DEPTH 6): one wave per SIMD, all registers
+  if (WM * WN == 4 && BM * BN >= 128 * 256) return 1;
   if (MODE != MODE_DGRAD || VAR != 3) return 2;
   if (BM == 64 && BN == 64) return 5;
   return (BM == 128 && BN == 128 && WM * WN == 8) ? 4 : 2;   // the others are at 2 (or 1) anyway
@@ -391,6 +416,18 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h = lane >> 4, c = lane & 15;
   const int wm = wv / WN, wn = wv % WN;
+  const bool trace_on = p.trace && blockIdx.x == 0 && lane == 0 && (wv == 0 || wv == 4);
+  auto stamp = [&](int slot) {
+    if (trace_on) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      __hip_atomic_store(&g_igemm_trace[(wv == 4) * kTraceSlots + slot], t, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  if (trace_on)
+    __hip_atomic_store(&g_igemm_trace[(wv == 4) * kTraceSlots + kTraceSlots - 5], __builtin_amdgcn_s_memrealtime(),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp(0);
 
   // ---- tile coordinates (XCD-aware) ----
   const int nwg = gridDim.x;
@@ -694,7 +731,9 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
 
   // LDS-DMA staging of one K-tile into LDS buffer `buf` (out-of-range chunks copy the zero page)
   auto issue_glds = [&](int k0, int buf) {
-    if (p.ablate & 2) return;
+    if constexpr (DEPTH != 6) {
+      if (p.ablate & 2) return;
+    }
     unsigned char* sa = smem + buf * T::STAGE;
     unsigned char* sb = sa + T::A_BYTES;
     if (MODE == MODE_WGRAD) {
@@ -708,9 +747,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         const bool ok = kk < k_end && co < p.M;
         SDX_DCHECK(!ok || (long)kk * g.K + co + 8 <= p.a_elems);
         const gptr16 src = ok ? (gptr16)(p.a + kk * g.K + co) : zp;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(sa + (wvu * T::A_CH + i) * 1024),
-                                         16, 0, 0);
+        glds16(src, sa + (wvu * T::A_CH + i) * 1024);
       }
       // B: im2col(x) rows (pixels) x BN (r, s, c) columns
 #pragma unroll
@@ -729,9 +766,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         }
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.b_elems));
         const gptr16 src = ok ? (gptr16)(p.b + off) : zp;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(sb + (wvu * T::B_CH + i) * 1024),
-                                         16, 0, 0);
+        glds16(src, sb + (wvu * T::B_CH + i) * 1024);
       }
       return;
     }
@@ -747,9 +782,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         const int off = rbase[i] + toff + lane_c;
         SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
         const gptr16 src = ok ? (gptr16)(p.a + off) : zp;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
-                                         16, 0, 0);
+        glds16(src, sa + 8 * (wvu * T::A_CH + i) * BK * 2);
       }
       const int kb = p.b_t0 + u_kr * p.b_tr + u_ks * p.b_ts + u_c0 + lane_c;
 #pragma unroll
@@ -757,9 +790,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         const bool ok = kok && b_off[i] >= 0;
         SDX_DCHECK(!ok || (long)b_off[i] + kb + 8 <= p.b_elems);
         const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + kb) : zp;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
-                                         16, 0, 0);
+        glds16(src, sb + 8 * (wvu * T::B_CH + i) * BK * 2);
       }
       u_c0 += BK;
       if (u_c0 == cdim) {
@@ -782,9 +813,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       const int off = a_rb[i] + toff;
       SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
       const gptr16 src = ok ? (gptr16)(p.a + off) : zp;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sa + 8 * (wvu * T::A_CH + i) * BK * 2),
-                                       16, 0, 0);
+      glds16(src, sa + 8 * (wvu * T::A_CH + i) * BK * 2);
     }
     const int kb = p.b_t0 + kr * p.b_tr + ks * p.b_ts + kc;
 #pragma unroll
@@ -792,14 +821,22 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       const bool ok = kok && b_off[i] >= 0;
       SDX_DCHECK(!ok || (long)b_off[i] + kb + 8 <= p.b_elems);
       const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + kb) : zp;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(sb + 8 * (wvu * T::B_CH + i) * BK * 2),
-                                       16, 0, 0);
+      glds16(src, sb + 8 * (wvu * T::B_CH + i) * BK * 2);
     }
     kc += BK;
-    while (kc >= cdim) {
-      kc -= cdim;
-      if (++ks == tap_s) { ks = 0; ++kr; }
+    if constexpr (DEPTH == 6) {
+      // cdim % BK == 0 (host routing): at most one wrap per K-tile, branch-free
+      const bool w1 = kc >= cdim;
+      kc = w1 ? kc - cdim : kc;
+      ks += w1 ? 1 : 0;
+      const bool w2 = ks == tap_s;
+      ks = w2 ? 0 : ks;
+      kr += w2 ? 1 : 0;
+    } else {
+      while (kc >= cdim) {
+        kc -= cdim;
+        if (++ks == tap_s) { ks = 0; ++kr; }
+      }
     }
   };
 
@@ -900,6 +937,22 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
           // D = Bᵀ·Aᵀ: accumulator column = output row (lane c), rows = output columns (4h + r)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[u][j], af[u][i], acc[i][j], 0, 0, 0);
   };
+  // one 32-deep k-step u of a K-tile (DEPTH 6 keeps two such sets in flight)
+  auto read_frags_u = [&](int buf, int u, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
+    const unsigned char* sa = smem + buf * T::STAGE;
+    const unsigned char* sb = sa + T::A_BYTES;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag_kin(sb, wn * WTN + 16 * j + c, u);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = frag_kin(sa, wm * WTM + 16 * i + c, u);
+  };
+  auto mfma_u = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
   auto compute = [&](int buf) {
     if (p.ablate & 4) return;
     bf16x8 af[2][TM], bfr[2][TN];
@@ -917,7 +970,56 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
   // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
   // issued a whole K-tile earlier (load latency covered by two tiles of MFMA work).
-  if constexpr (DEPTH == 5) {
+  if constexpr (DEPTH == 6) {
+    // One wave per SIMD (4-wave block, 64x128 / 128x64 wave tiles: half the LDS fragment
+    // bytes per MFMA of the 8-wave 64x32 tiles) over a 3-buffer LDS-DMA ring, pipelined
+    // inside each wave. A K-tile is two 32-deep k-steps: the fragments of step 1 are read
+    // while step 0's MFMAs run, then ONE raw barrier (every wave's reads of this tile are
+    // done and its own DMAs of tile k+1 retired by the counted vmcnt), then the buffer just
+    // freed is refilled with tile k+3 and step 0 of tile k+1 is read, both interleaved with
+    // step 1's MFMAs — the matrix pipe idles only for the barrier.
+    // RAW: tile k+1 is read after the barrier of iteration k, which every wave reaches after
+    // retiring its own DMAs of tile k+1. WAR: tile k+3 overwrites tile k's buffer only after
+    // that barrier, which every wave reaches after its last read of tile k completed
+    // (lds_barrier: lgkmcnt(0)). The DMA issue is unconditional (tiles past the end load the
+    // zero page into the free buffer and are never read; host routing guarantees
+    // cdim % BK == 0, so the k decode advances branch-free), keeping the second half one
+    // basic block for the MFMA/DMA interleave; the queue is drained after the loop.
+    constexpr int NL = T::A_CH + T::B_CH;   // LDS-DMA instructions per wave per tile
+    bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+    issue_glds(k_begin, 0);
+    issue_glds(k_begin + BK, 1);
+    issue_glds(k_begin + 2 * BK, 2);
+    vm_wait<2 * NL>();
+    lds_barrier();
+    stamp(1);
+    read_frags_u(0, 0, a0, b0);
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      read_frags_u(buf, 1, a1, b1);
+      mfma_u(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt < 160) stamp(2 + 3 * kt);
+      vm_wait<NL>();   // own DMAs of tile kt+1 retired; tile kt+2 stays in flight
+      lds_barrier();
+      if (kt < 160) stamp(3 + 3 * kt);
+      const int nbuf = buf == 2 ? 0 : buf + 1;
+      read_frags_u(nbuf, 0, a0, b0);
+      issue_glds(k_begin + (kt + 3) * BK, buf);
+      mfma_u(a1, b1);
+      // the DMA issue (address VALU + LDS-DMA) interleaved with the second half's MFMAs
+      // instead of ahead of them (the matrix pipe would idle through it)
+      if constexpr (SDX_W1_SGB) static_for<0, TM * TN>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // up to 5 VALU
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // up to 1 VMEM read (LDS-DMA)
+        __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);   // up to 2 SALU
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      buf = nbuf;
+    }
+    vm_wait<0>();   // zero-page DMAs past the end land before the epilogue reuses the LDS
+  } else if constexpr (DEPTH == 5) {
     // Ping-pong over a 3-buffer LDS-DMA ring (8-wave blocks, one per CU). Every wave
     // alternates a LOAD segment (the fragment ds_reads of tile k into registers, then its
     // share of tile k+2's LDS-DMA) and a COMPUTE segment (tile k's MFMAs on those
@@ -941,6 +1043,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     vm_wait<NL>();
     lds_barrier();
     if (late) lds_barrier();
+    stamp(1);
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
       bf16x8 af[2][TM], bfr[2][TN];
@@ -961,12 +1064,15 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       // the very next segment (a wait placed after the MFMAs would be too late for group 1's
       // share, which group 0 reads during group 1's compute segment)
       if (more) vm_wait<NL>(); else vm_wait<0>();
+      if (kt < 160) stamp(2 + 3 * kt);
       lds_barrier();
+      if (kt < 160) stamp(3 + 3 * kt);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
       if (!(p.ablate & 4)) mfma_tile(af, bfr);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
+      if (kt < 160) stamp(4 + 3 * kt);
       __builtin_amdgcn_s_barrier();
       buf = buf == 2 ? 0 : buf + 1;
     }
@@ -1040,6 +1146,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     }
   }
 
+  stamp(kTraceSlots - 4);
   // ---------------------------------- epilogues ----------------------------------
   // acc[i][j][r] = C[m0 + wm*64 + 16i + c][n0 + wn*64 + 16j + 4h + r]
   // (not compiled into the BN-statistics DGRAD variant: its register budget sits at the
@@ -1193,6 +1300,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         *reinterpret_cast<uint2*>(smem + (wm * WTM + 16 * i + c) * CRS + (wn * WTN + 16 * j + 4 * h) * 2) = ov[i][j];
   }
   __syncthreads();
+  stamp(kTraceSlots - 3);
   // fused BN-backward statistics (DGRAD): per-thread sums for column chunk my_ch
   const int bs_ns = p.bs.yb != nullptr ? 3 : 2;
   float bmu_a[8], bmu_b[8], bmk_s[8], bmk_t[8], bsum[3][8];
@@ -1387,6 +1495,10 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     }
     if constexpr (SF) stat_fuse_tail<NT, BN, 2>(p.sf, p.stats, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
   }
+  stamp(kTraceSlots - 2);
+  if (trace_on)
+    __hip_atomic_store(&g_igemm_trace[(wv == 4) * kTraceSlots + kTraceSlots - 1], __builtin_amdgcn_s_memrealtime(),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // dW = Σ_split partial[split] (fp32); optional accumulate into dW. A block owns 64 float4
@@ -1448,6 +1560,14 @@ int igemm_glds() {
   return a;
 }
 
+int igemm_trace_on() {
+  static const int v = [] {
+    const char* e = getenv("SDX_IGEMM_TRACE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int igemm_ablate() {
   static const int a = [] {
     const char* e = getenv("SDX_IGEMM_ABLATE");
@@ -1465,11 +1585,12 @@ int igemm_ring() {
   return v;
 }
 
-// ping-pong main loop of the 8-wave 256x128 / 128x256 tiles (SDX_IGEMM_PP=0: DEPTH 3 instead)
+// main loop of the 8-wave 256x128 / 128x256 tiles: 0 DEPTH 3, 1 ping-pong (DEPTH 5), 2 in-wave
+// pipelined (DEPTH 6, default)
 int igemm_pp() {
   static const int v = [] {
     const char* e = getenv("SDX_IGEMM_PP");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -1509,7 +1630,7 @@ template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   // LDS-DMA main loops (DEPTH 3: two buffers; 5: ping-pong ring) carry every epilogue
   // variant; the single-stage (ONE) form is DEPTH 3 at one K-tile
-  constexpr bool GLK = (DEPTH == 3 || DEPTH == 5) && MODE != MODE_WGRAD;
+  constexpr bool GLK = (DEPTH == 3 || DEPTH == 5 || DEPTH == 6) && MODE != MODE_WGRAD;
   const bool one = DEPTH == 3 && p.Kdim <= BK && igemm_one();
   if (MODE == MODE_FWD && p.bn_sc != nullptr) {
     // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
@@ -1555,6 +1676,7 @@ hipError_t launch_w(int grid, const IgemmParams& p, hipStream_t s) {
 template <int MODE, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   p.ablate = igemm_ablate();
+  p.trace = igemm_trace_on();
   p.m_tiles = (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
   const int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
@@ -1575,19 +1697,32 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   {
     // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
     // (SDX_IGEMM_GLDS=2 enables it there too)
-    // ping-pong main loop: the 8-wave 256x128 / 128x256 tiles at more than two K-tiles
+    // 256x128 / 128x256 tiles at more than two K-tiles: the 8-wave ones run the ping-pong
+    // loop (DEPTH 5, SDX_IGEMM_PP=1) or the in-wave pipelined loop (DEPTH 6, SDX_IGEMM_PP=2,
+    // default); the 4-wave ones (64x128 / 128x64 wave tiles) DEPTH 6
     constexpr bool kPP = WM * WN == 8 && BM * BN == 256 * 128;
-    const bool pp = kPP && igemm_pp() && p.Kdim > 2 * BK && p.in_scale == nullptr;
+    constexpr bool kW1 = BM * BN >= 128 * 256;
+    const bool pp = kPP && igemm_pp() == 1 && p.Kdim > 2 * BK && p.in_scale == nullptr;
+    // the channel dim of the K decode (FWD C, DGRAD K) a multiple of BK: branch-free advance
+    const int cdim_h = MODE == MODE_FWD ? p.g.C : p.g.K;
+    const bool w1 = kW1 && (WM * WN == 4 || igemm_pp() == 2) && p.Kdim > 2 * BK && p.in_scale == nullptr &&
+                    cdim_h % BK == 0;
     if (p.sf.cnt != nullptr) {
       if (p.in_scale != nullptr) return hipErrorInvalidValue;
       if constexpr (kPP) {
         if (pp) return launch_k<MODE, BM, BN, WM, WN, 5>(bs, grid, p, s);
+      }
+      if constexpr (kW1 && MODE != MODE_WGRAD) {
+        if (w1) return launch_k<MODE, BM, BN, WM, WN, 6>(bs, grid, p, s);
       }
       return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
     }
     if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
       if constexpr (kPP) {
         if (pp) return launch_k<MODE, BM, BN, WM, WN, 5>(bs, grid, p, s);
+      }
+      if constexpr (kW1 && MODE != MODE_WGRAD) {
+        if (w1) return launch_k<MODE, BM, BN, WM, WN, 6>(bs, grid, p, s);
       }
       if constexpr (MODE != MODE_WGRAD) {
         if (igemm_ring() && p.Kdim > 2 * BK) return launch_k<MODE, BM, BN, WM, WN, 4>(bs, grid, p, s);
@@ -1609,7 +1744,9 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
 // tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
 // 4 128x128 with 8 waves (2x4 of 64x32: twice the waves per SIMD for latency hiding),
 // 5 256x128 with 8 waves (4x2 of 64x64, one block per CU), 6 128x256 with 8 waves (2x4 of
-// 64x64); both run the ping-pong main loop (DEPTH 5, 144 KiB LDS ring) at K > 128
+// 64x64); both run the ping-pong main loop (DEPTH 5, 144 KiB LDS ring) at K > 128;
+// 7 128x256 / 8 256x128 with 4 waves (2x2 of 64x128 / 128x64, one wave per SIMD), the in-wave
+// pipelined loop (DEPTH 6) at K > 128
 template <int MODE>
 hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
   switch (cfg) {
@@ -1620,6 +1757,8 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
     case 4: return launch_cfg<MODE, 128, 128, 2, 4>(p, s);
     case 5: return launch_cfg<MODE, 256, 128, 4, 2>(p, s);
     case 6: return launch_cfg<MODE, 128, 256, 2, 4>(p, s);
+    case 7: return launch_cfg<MODE, 128, 256, 2, 2>(p, s);
+    case 8: return launch_cfg<MODE, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1627,11 +1766,11 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
 }  // namespace
 
 int igemm_tile_m(int cfg) {
-  static const int m[7] = {128, 256, 64, 64, 128, 256, 128};
+  static const int m[9] = {128, 256, 64, 64, 128, 256, 128, 128, 256};
   return m[cfg];
 }
 int igemm_tile_n(int cfg) {
-  static const int n[7] = {128, 64, 256, 64, 128, 128, 256};
+  static const int n[9] = {128, 64, 256, 64, 128, 128, 256, 256, 128};
   return n[cfg];
 }
 
@@ -1806,3 +1945,12 @@ hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float
 // the BN-apply epilogue runs on the LDS-DMA tiles (DEPTH 3), not the register-staged or
 // ring variants
 bool conv_fwd_bnapply_supported() { return igemm_glds() != 0 && !igemm_ring(); }
+
+// the diagnostic timeline of the last traced launch (SDX_IGEMM_TRACE=1): 2 x kTraceSlots u64
+int igemm_trace_slots() { return kTraceSlots; }
+hipError_t igemm_trace_copy(unsigned long long* host, hipStream_t s) {
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_igemm_trace), sizeof(unsigned long long) * 2 * kTraceSlots, 0,
+                             hipMemcpyDeviceToHost);
+}
