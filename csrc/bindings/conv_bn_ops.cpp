@@ -80,6 +80,15 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
   // and epilogue latency); on the K=64 layer-1 GEMMs its longer prologue costs more than it
   // hides. wgrad keeps the 4-wave tiles (its split-K slabs are short). profiles/conv_cfg4_r1.txt
   if (fill && best == 0 && Kdim >= 128) best = 4;
+  // long-K GEMMs whose output width is a multiple of 256 (layers 3-4): the 8-wave 128x256 tile
+  // on the in-wave pipelined LDS-DMA ring (cfg 6, DEPTH 6) — l3 3x3 fwd/dgrad 41.3 -> 38.1 us,
+  // l4.0.sc dgrad 67.5 -> 64.8 us; it loses on narrower or short-K GEMMs, where one tile per CU
+  // leaves its prologue/epilogue exposed (profiles/conv_core_r4.txt)
+  static const bool d6 = [] {
+    const char* e = getenv("SDX_CONV_D6");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (fill && d6 && Ncol % 256 == 0 && Kdim >= 1024) best = 6;
   return best;
 }
 

@@ -46,6 +46,9 @@ constexpr int BK = 64;
 #ifndef SDX_FRAG_PIN
 #define SDX_FRAG_PIN 0
 #endif
+#ifndef SDX_W1_ABL
+#define SDX_W1_ABL 0   // DEPTH 6: honour the SDX_IGEMM_ABLATE bits (diagnostic builds only)
+#endif
 #ifndef SDX_W1_SGB
 #define SDX_W1_SGB 1   // DEPTH 6: sched_group_barrier interleave of the second half
 #endif
@@ -523,7 +526,10 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   // wave-uniform: per-row validity over all taps is precomputed as a bitmask and a chunk
   // address is row base + uniform tap offset + lane constant (no per-chunk multiplies).
   const int taps = (MODE == MODE_FWD) ? g.R * g.S : p.nr * p.ns;
-  const bool fast_taps = SDX_FAST_TAPS && GL && MODE != MODE_WGRAD && (cdim % BK) == 0 && taps <= 32;
+  // (always on in DEPTH 6, whose host routing guarantees cdim % BK == 0 and taps <= 32: it
+  // halves the address VALU of the DMA issue, which is interleaved with the MFMAs there)
+  const bool fast_taps = (DEPTH == 6 && MODE != MODE_WGRAD) ||
+                         (SDX_FAST_TAPS && GL && MODE != MODE_WGRAD && (cdim % BK) == 0 && taps <= 32);
   constexpr int FCH = (GL && MODE != MODE_WGRAD) ? T::A_CH : 1;
   unsigned vmask[FCH];
   int rbase[FCH];
@@ -771,7 +777,8 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       return;
     }
     const int k = k0 + kin_ch * 8;
-    const bool kok = k < k_end;
+    // DEPTH 6: K-tiles never straddle k_end (Kdim % BK == 0), so the test is wave-uniform
+    const bool kok = DEPTH == 6 ? k0 < k_end : k < k_end;
     if (fast_taps) {
       const int tap = u_kr * tap_s + u_ks;
       const int toff = (MODE == MODE_FWD) ? (u_kr * g.W + u_ks) * g.C + u_c0 : -(u_kr * g.Q + u_ks) * g.K + u_c0;
@@ -793,7 +800,15 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         glds16(src, sb + 8 * (wvu * T::B_CH + i) * BK * 2);
       }
       u_c0 += BK;
-      if (u_c0 == cdim) {
+      if constexpr (DEPTH == 6) {
+        // branch-free (keeps the DMA issue in the MFMA basic block)
+        const bool w1 = u_c0 == cdim;
+        u_c0 = w1 ? 0 : u_c0;
+        u_ks += w1 ? 1 : 0;
+        const bool w2 = u_ks == tap_s;
+        u_ks = w2 ? 0 : u_ks;
+        u_kr += w2 ? 1 : 0;
+      } else if (u_c0 == cdim) {
         u_c0 = 0;
         if (++u_ks == tap_s) { u_ks = 0; ++u_kr; }
       }
@@ -996,17 +1011,17 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     read_frags_u(0, 0, a0, b0);
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      read_frags_u(buf, 1, a1, b1);
-      mfma_u(a0, b0);
+      if (!(SDX_W1_ABL && (p.ablate & 8))) read_frags_u(buf, 1, a1, b1);
+      if (!(SDX_W1_ABL && (p.ablate & 4))) mfma_u(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
       if (kt < 160) stamp(2 + 3 * kt);
       vm_wait<NL>();   // own DMAs of tile kt+1 retired; tile kt+2 stays in flight
       lds_barrier();
       if (kt < 160) stamp(3 + 3 * kt);
       const int nbuf = buf == 2 ? 0 : buf + 1;
-      read_frags_u(nbuf, 0, a0, b0);
-      issue_glds(k_begin + (kt + 3) * BK, buf);
-      mfma_u(a1, b1);
+      if (!(SDX_W1_ABL && (p.ablate & 8))) read_frags_u(nbuf, 0, a0, b0);
+      if (!(SDX_W1_ABL && (p.ablate & 2))) issue_glds(k_begin + (kt + 3) * BK, buf);
+      if (!(SDX_W1_ABL && (p.ablate & 4))) mfma_u(a1, b1);
       // the DMA issue (address VALU + LDS-DMA) interleaved with the second half's MFMAs
       // instead of ahead of them (the matrix pipe would idle through it)
       if constexpr (SDX_W1_SGB) static_for<0, TM * TN>([&](auto) {
@@ -1705,8 +1720,9 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
     const bool pp = kPP && igemm_pp() == 1 && p.Kdim > 2 * BK && p.in_scale == nullptr;
     // the channel dim of the K decode (FWD C, DGRAD K) a multiple of BK: branch-free advance
     const int cdim_h = MODE == MODE_FWD ? p.g.C : p.g.K;
+    const int taps_h = MODE == MODE_FWD ? p.g.R * p.g.S : p.nr * p.ns;
     const bool w1 = kW1 && (WM * WN == 4 || igemm_pp() == 2) && p.Kdim > 2 * BK && p.in_scale == nullptr &&
-                    cdim_h % BK == 0;
+                    cdim_h % BK == 0 && taps_h <= 32;
     if (p.sf.cnt != nullptr) {
       if (p.in_scale != nullptr) return hipErrorInvalidValue;
       if constexpr (kPP) {

@@ -51,10 +51,39 @@ def main():
     grad = eng.flat.grad.detach().clone()
     eng.optimizer.step()
     torch.cuda.synchronize()
+
+    def state_hash():
+        # exact replica fingerprint: every parameter and every BN running statistic, bit for bit
+        flat = eng.flat.flat.detach().view(torch.int32).to(torch.int64)
+        bufs = [b.detach().reshape(-1).float().view(torch.int32).to(torch.int64) for b in eng.model.buffers()
+                if b.is_floating_point()]
+        w = torch.arange(1, flat.numel() + 1, device=flat.device, dtype=torch.int64)
+        hf = int((flat * w).sum()) & ((1 << 62) - 1)
+        hb = int(sum(int((t * torch.arange(1, t.numel() + 1, device=t.device, dtype=torch.int64)).sum()) for t in bufs))
+        return hf, hb & ((1 << 62) - 1)
+
+    hashes = [state_hash()]
+    # SDX_TEST_STEPS > 1: further steps on fresh data (replicas and running statistics must stay
+    # bit-identical across ranks after every step; >300 SyncBN exchanges at ResNet-50 x 3 steps)
+    for step in range(1, int(os.environ.get("SDX_TEST_STEPS", "1"))):
+        gs = torch.Generator().manual_seed(7 + step)
+        im = torch.randn(2, G, 3, 32, 32, generator=gs)
+        xs = torch.cat([im[0, sl], im[1, sl]]).cuda()
+        fs = eng.runner.forward(to_nhwc_input(xs) if eng.backend == "native" else xs)
+        ls = eng.criterion(fs)
+        eng.optimizer.zero_grad()
+        ls.backward()
+        if eng.reducer is not None:
+            eng.reducer.finish()
+        eng.optimizer.step()
+        torch.cuda.synchronize()
+        hashes.append(state_hash())
     bn = eng.model.encoder.layer1[0].bn1
-    torch.save({"flat": eng.flat.flat.detach().cpu(), "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
+    torch.save({"hashes": hashes, "flat": eng.flat.flat.detach().cpu() if len(hashes) == 1 else None,
+                "rm": bn.running_mean.cpu(), "rv": bn.running_var.cpu(),
                 "native_h": comm.native_small_comm(None), "loss": float(loss.detach()), "grad": grad.cpu(), "names": list(eng.flat.names),
                 "offsets": [int(o) for o in eng.flat.offsets], "numels": [p.numel() for p in eng.flat.params]}, os.path.join(out_dir, f"{name}_w{world}{os.environ.get('SDX_TEST_GRAD_COMPRESS', '')}_r{rank}.pt"))
+    print(f"rank {rank}: state hashes per step {hashes}")
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -21,13 +21,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _launch(world, out, syncbn_comm="", model="resnet18", compress=""):
+def _launch(world, out, syncbn_comm="", model="resnet18", compress="", steps=1):
     # file-store rendezvous: no probed TCP port that another job on the box can take first
     rdv = os.path.join(str(out), f"rdv_{model}_{world}_{syncbn_comm or 'pg'}{compress}")
     procs = []
     for r in range(world):
         env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, SDX_TEST_MODEL=model, RANK=str(r), LOCAL_RANK="0",
-                   SDX_TEST_GRAD_COMPRESS=compress,
+                   SDX_TEST_GRAD_COMPRESS=compress, SDX_TEST_STEPS=str(steps),
                    WORLD_SIZE=str(world), SDX_CONV_CFG="4",
                    MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD="file://" + rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
@@ -103,3 +103,34 @@ def test_two_rank_bf16_compressed_gradients(gpu, tmp_path):
                 for o, k in zip(a["offsets"], a["numels"]))
     print(f"bf16-compressed W=2 vs W=1: worst parameter-gradient rel {worst:.3g}")
     assert worst < 5e-2, worst
+
+
+def test_four_rank_resnet50_fused_syncbn_three_steps(gpu, tmp_path):
+    """W=4 ResNet-50 in four real processes on this GPU (gloo process group + the fused xGMI
+    SyncBN arena, the path an 8-GPU node takes with --syncbn_comm xgmi): step 1's every
+    parameter gradient matches the W=1 step on the concatenated batch, and over three
+    consecutive steps (>300 fused SyncBN exchanges: the arena's epoch/parity wrap) every
+    rank's parameters and BN running statistics stay bit-identical after each step
+    (reference: main_supcon.py:222-234, :268-281)."""
+    _launch(1, tmp_path, "", "resnet50")
+    _launch(4, tmp_path, "xgmi", "resnet50", steps=3)
+    ref = torch.load(tmp_path / "resnet50_w1_r0.pt", weights_only=True)
+    ranks = [torch.load(tmp_path / f"resnet50_w4_r{r}.pt", weights_only=True) for r in range(4)]
+    assert all(d["native_h"] > 0 for d in ranks), "xGMI small communicator was not registered"
+    a = ranks[0]
+    worst = []
+    for n, o, k in zip(a["names"], a["offsets"], a["numels"]):
+        g1, g4 = ref["grad"][o:o + k].double(), a["grad"][o:o + k].double()
+        worst.append((float((g4 - g1).norm() / (g1.norm() + 1e-12)), n))
+    worst.sort(reverse=True)
+    med = sorted(r for r, _ in worst)[len(worst) // 2]
+    print(f"resnet50 W=4 (xgmi fused) vs W=1: median grad rel {med:.3g}, worst "
+          + ", ".join(f"{n} {r:.3g}" for r, n in worst[:4]))
+    print("per-step state hashes (rank 0):", a["hashes"])
+    for d in ranks[1:]:
+        assert torch.equal(d["grad"], a["grad"]), "all-reduced step-1 gradients differ across ranks"
+        assert d["hashes"] == a["hashes"], (d["hashes"], a["hashes"])   # replicas + BN stats, every step
+    assert len(a["hashes"]) == 3
+    assert abs(sum(d["loss"] for d in ranks) - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3
+    assert med < 2e-2, med
+    assert worst[0][0] < 6e-2, worst[:8]

@@ -45,6 +45,20 @@ def main():
         print(f"wave {4 * g}: total {cyc} cycles, {rt * 1e6:.2f} us -> {cyc / rt / 1e9 if rt else 0:.2f} GHz; "
               f"prologue {r[1] - t0}, loop {r[S - 4] - r[1]}, epilogue {r[S - 2] - r[S - 4]} "
               f"(staged at +{r[S - 3] - r[S - 4]})")
+        if r[4] == 0 and r[2] > 0:
+            # DEPTH 6 stamps only E2 (first-half MFMAs issued) and E3 (after the barrier)
+            rows = []
+            kt = 0
+            while 2 + 3 * (kt + 1) < S - 5 and r[2 + 3 * (kt + 1)] > 0 and kt < 159:
+                rows.append((r[3 + 3 * kt] - r[2 + 3 * kt], r[2 + 3 * (kt + 1)] - r[3 + 3 * kt]))
+                kt += 1
+            if rows:
+                n = len(rows)
+                print(f"  {n} K-tiles: vmcnt+barrier wait {sum(x[0] for x in rows) / n:.0f}  "
+                      f"half2 + next half1 {sum(x[1] for x in rows) / n:.0f} cycles (mean)")
+                for x in rows[:4] + rows[-3:]:
+                    print("   ", x)
+            continue
         rows = []
         kt = 0
         while 4 + 3 * kt < S - 5 and r[4 + 3 * kt] > 0 and kt < 160:
