@@ -15,6 +15,7 @@ namespace {
 
 struct Arena {
   bool emulated = false;           // W virtual ranks' arenas in this device's memory (tests)
+  bool solo = false;               // emulated: one rank's share only (XgmiCol::solo)
   int device = 0;
   int rank = 0;
   int world = 1;
@@ -149,6 +150,10 @@ int64_t xgmi_emu_create(int64_t world, int64_t cap, double timeout_s) {
   TORCH_CHECK(cap > 0 && cap <= (1 << 20), "cap in (0, 2^20]");
   auto a = std::make_unique<Arena>();
   a->emulated = true;
+  {
+    const char* e = getenv("SDX_SYNCBN_EMU_SOLO");
+    a->solo = e != nullptr && atoi(e) != 0;
+  }
   check_hip(hipGetDevice(&a->device), "hipGetDevice");
   a->world = (int)world;
   a->cap = (size_t)cap;
@@ -213,6 +218,7 @@ XgmiCol xgmi_col_args(int64_t id) {
   x.err = a.err;
   x.timeout_ticks = a.timeout_ticks;
   x.slab_zstride = 0;
+  x.solo = a.solo ? 1 : 0;
   return x;
 }
 bool xgmi_emulated(int64_t id) { return get(id).emulated; }
@@ -230,7 +236,7 @@ torch::Tensor xgmi_exchange_sums(int64_t id, torch::Tensor slab, double timeout_
   XgmiCol x = xgmi_col_args(id);
   x.timeout_ticks = call_ticks(get(id), timeout_s);
   c10::DeviceGuard dg(slab.device());
-  const int z = x.mode == 2 ? x.world : 1;
+  const int z = x.mode == 2 && !x.solo ? x.world : 1;
   auto sums = torch::empty({nsets, C}, slab.options().dtype(at::kDouble));
   auto scratch = reduce_scratch(slab, rows, nsets, C, z);
   check_hip(launch_col_reduce(slab.data_ptr<float>(), (int)rows, (int)nsets, (int)C, scratch.data_ptr<double>(),

@@ -24,7 +24,7 @@ torch::Tensor reduce_scratch(const torch::Tensor& like, int64_t rows, int64_t ns
 struct FusedX {
   XgmiCol x{};
   bool on = false;
-  int z() const { return on && x.mode == 2 ? x.world : 1; }
+  int z() const { return on && x.mode == 2 && !x.solo ? x.world : 1; }
   const XgmiCol* p() const { return on ? &x : nullptr; }
 };
 FusedX fused_exchange(int64_t comm);

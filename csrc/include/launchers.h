@@ -200,6 +200,11 @@ struct XgmiCol {
   int* err = nullptr;               // host-pinned: 1 + sender whose flag missed the deadline
   long long timeout_ticks = 0;      // 100 MHz wall-clock ticks
   long slab_zstride = 0;            // mode 2: elements between virtual ranks' slabs
+  // mode 2, one rank's share (SDX_SYNCBN_EMU_SOLO / tools/syncbn_latency.py): only virtual
+  // rank 0 runs (grid z = 1); it reduces, stores to all W arenas, publishes all W flags and
+  // polls only its own flag — the other W-1 ranks count as already published — so the
+  // kernel time is one real rank's reduce + W stores + poll + W-slot sum + epilogue
+  int solo = 0;
 };
 
 // Deterministic reduction of a [rows][nsets][C] fp32 slab to fp64 sums [nsets][C] in ONE

@@ -47,8 +47,12 @@ namespace {
 // and polls its own W flags of group x against the wall-clock deadline. The slots are
 // then summed in rank order, so every rank holds bit-identical global sums, and the
 // epilogue (finalize / coefficients, with the global count) runs on them. Every 64-channel
-// group is an independent instance of the two-parity protocol of xgmi.hip, and no block
-// waits on another block of its own launch, so the kernel cannot deadlock on itself.
+// group is an independent instance of the two-parity protocol of xgmi.hip. With real peers
+// (mode 1) no block waits on another block of its own launch. In the single-GPU emulation
+// (mode 2) virtual rank z's last block of group x DOES spin on the other ranks' last blocks
+// of the same launch, so progress needs them co-resident: launch_col_reduce bounds the
+// spinners (groups x W <= 512, far below the 256-CU residency) — solo mode (one rank's
+// share) polls only its own flag.
 template <int NS, int XG>
 __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, int me) {
   constexpr int kScope = XG == 1 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
@@ -69,7 +73,8 @@ __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's data stores are acknowledged
   if (threadIdx.x == 0) ok = 1;
   __syncthreads();
-  if (threadIdx.x < W) {   // wave 0: the same wave that stored the data, after its drain
+  if (threadIdx.x < W && !(XG == 2 && xg.solo && threadIdx.x != me)) {
+    // wave 0: the same wave that stored the data, after its drain
     const int p = threadIdx.x;
     __hip_atomic_store(xg.peers.flags[p] + ((size_t)par * W + me) * kXgmiFlagGroups + blockIdx.x, xg.epoch,
                        __ATOMIC_RELAXED, kScope);
@@ -571,7 +576,10 @@ hipError_t launch_col_reduce(const float* slab, int rows, int nsets, int C, doub
              (size_t)nsets * C > xg->peers.cap || (C + 63) / 64 > kXgmiFlagGroups || xg->timeout_ticks <= 0))
     return hipErrorInvalidValue;
   if (xg && xm == 2 && xg->slab_zstride < 0) return hipErrorInvalidValue;
-  const dim3 grid((C + 63) / 64, col_reduce_gy(rows), xm == 2 ? xg->world : 1), blk(256);
+  // emulation: the spinning last blocks (one per group and virtual rank) must stay co-resident
+  if (xg && xm == 2 && !xg->solo && ((C + 63) / 64) * xg->world > 512) return hipErrorInvalidValue;
+  if (xg && xg->solo && (xm != 2 || xg->me != 0)) return hipErrorInvalidValue;
+  const dim3 grid((C + 63) / 64, col_reduce_gy(rows), xm == 2 && !xg->solo ? xg->world : 1), blk(256);
   const BnFinalizeArgs f = fa ? *fa : BnFinalizeArgs{};
   const BnCoefArgs k = ca ? *ca : BnCoefArgs{};
   const XgmiCol x = xg ? *xg : XgmiCol{};

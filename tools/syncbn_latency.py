@@ -14,8 +14,12 @@ images x 2 views per GPU) it times, with HIP events over back-to-back calls:
              rank-ordered sum, all in ONE launch. The W virtual ranks share this GPU, so
              it also pays W x the reduction work of one rank (upper bound of the real
              per-rank cost, minus the xGMI link latency of the real peers).
+* solo     — ONE rank's share of the fused exchange (SDX_SYNCBN_EMU_SOLO arena): only virtual
+             rank 0 runs; it reduces its slab, stores into all W arenas, publishes all W flags,
+             polls its own flag (the other ranks count as published) and sums the W slots — the
+             per-rank kernel cost of a real W-GPU run minus the xGMI hop latency.
 
-python tools/syncbn_latency.py [W] [iters]
+python tools/syncbn_latency.py [W[,W...]] [iters]     (default 2,4,8)
 """
 import os
 import sys
@@ -42,48 +46,61 @@ def _time(fn, iters):
 
 
 def main():
-    W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    Ws = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "2,4,8").split(",")]
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
     dev = torch.device("cuda:0")
-    he = m.emu_small_comm(W)
-    hx = m.xgmi_emu_small_comm(W)
-    print(f"per-BN SyncBN cost, W = {W} emulated ranks on one GPU, {iters} back-to-back calls (µs per BN)")
-    print(f"{'C':>6} {'rows':>6} | {'local':>8} {'3-launch':>9} {'fused':>8} | fused - local")
-    tot = {"local": 0.0, "emu3": 0.0, "fused": 0.0}
-    for C, rows in SHAPES:
-        slab = torch.randn(rows, 2, C, device=dev).abs_()
-        g = torch.ones(C, device=dev)
-        b = torch.zeros(C, device=dev)
-        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
-        cnt = float(rows * 128)
-        args = (g, b, 1e-5, 0.1, True, rm, rv)
+    summary = []
+    for W in Ws:
+        he = m.emu_small_comm(W)
+        hx = m.xgmi_emu_small_comm(W)
+        os.environ["SDX_SYNCBN_EMU_SOLO"] = "1"
+        hs = m.xgmi_emu_small_comm(W)
+        del os.environ["SDX_SYNCBN_EMU_SOLO"]
+        print(f"per-BN SyncBN cost, W = {W} emulated ranks on one GPU, {iters} back-to-back calls (us per BN)")
+        print(f"{'C':>6} {'rows':>6} | {'local':>8} {'3-launch':>9} {'fused':>8} {'solo':>8} | solo - local")
+        tot = {"local": 0.0, "emu3": 0.0, "fused": 0.0, "solo": 0.0}
+        for C, rows in SHAPES:
+            slab = torch.randn(rows, 2, C, device=dev).abs_()
+            g = torch.ones(C, device=dev)
+            b = torch.zeros(C, device=dev)
+            rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+            cnt = float(rows * 128)
+            args = (g, b, 1e-5, 0.1, True, rm, rv)
 
-        def local():
-            m.bn_stats_finalize(slab, cnt, *args)
+            def local():
+                m.bn_stats_finalize(slab, cnt, *args)
 
-        def emu3():
-            s = m.bn_stats_reduce(slab)
-            m.small_all_reduce_(he, s)
-            m.bn_finalize(s, cnt * W, *args)
+            def emu3():
+                s_ = m.bn_stats_reduce(slab)
+                m.small_all_reduce_(he, s_)
+                m.bn_finalize(s_, cnt * W, *args)
 
-        def fused():
-            m.syncbn_exchange_sums(hx, slab)
+            def fused():
+                m.syncbn_exchange_sums(hx, slab)
 
-        t = {k: _time(f, iters) for k, f in (("local", local), ("emu3", emu3), ("fused", fused))}
-        ref = slab.double().sum(0) * W
-        got = m.syncbn_exchange_sums(hx, slab)
-        torch.cuda.synchronize()
-        assert torch.allclose(got, ref, rtol=1e-12, atol=1e-9), "fused exchange mismatch"
-        for k in tot:
-            tot[k] += t[k]
-        print(f"{C:>6} {rows:>6} | {t['local']:8.2f} {t['emu3']:9.2f} {t['fused']:8.2f} | {t['fused'] - t['local']:+7.2f}")
-    n = len(SHAPES)
-    print(f"{'mean':>13} | {tot['local'] / n:8.2f} {tot['emu3'] / n:9.2f} {tot['fused'] / n:8.2f} | "
-          f"{(tot['fused'] - tot['local']) / n:+7.2f}")
-    m.small_comm_destroy(he)
-    m.small_comm_destroy(hx)
+            def solo():
+                m.syncbn_exchange_sums(hs, slab)
+
+            t = {k: _time(f, iters) for k, f in (("local", local), ("emu3", emu3), ("fused", fused), ("solo", solo))}
+            ref = slab.double().sum(0) * W
+            got = m.syncbn_exchange_sums(hx, slab)
+            torch.cuda.synchronize()
+            assert torch.allclose(got, ref, rtol=1e-12, atol=1e-9), "fused exchange mismatch"
+            for k in tot:
+                tot[k] += t[k]
+            print(f"{C:>6} {rows:>6} | {t['local']:8.2f} {t['emu3']:9.2f} {t['fused']:8.2f} {t['solo']:8.2f} | "
+                  f"{t['solo'] - t['local']:+7.2f}")
+        n = len(SHAPES)
+        print(f"{'mean':>13} | {tot['local'] / n:8.2f} {tot['emu3'] / n:9.2f} {tot['fused'] / n:8.2f} "
+              f"{tot['solo'] / n:8.2f} | {(tot['solo'] - tot['local']) / n:+7.2f}")
+        summary.append((W, tot["local"] / n, tot["emu3"] / n, tot["fused"] / n, tot["solo"] / n))
+        for h in (he, hx, hs):
+            m.small_comm_destroy(h)
+    print("summary (mean us per BN): W local 3-launch fused solo")
+    for r in summary:
+        print("  %d %8.2f %8.2f %8.2f %8.2f" % r)
 
 
 if __name__ == "__main__":
