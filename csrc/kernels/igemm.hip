@@ -1033,7 +1033,10 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       __builtin_amdgcn_sched_barrier(0);
       buf = nbuf;
     }
-    vm_wait<0>();   // zero-page DMAs past the end land before the epilogue reuses the LDS
+    // the zero-page DMAs issued past the end must land before ANY wave's epilogue reuses the
+    // LDS (C staging): this wave's drain, then a barrier behind every wave's drain
+    vm_wait<0>();
+    __syncthreads();
   } else if constexpr (DEPTH == 5) {
     // Ping-pong over a 3-buffer LDS-DMA ring (8-wave blocks, one per CU). Every wave
     // alternates a LOAD segment (the fragment ds_reads of tile k into registers, then its

@@ -408,6 +408,11 @@ class PretrainEngine:
         exactly the eager trajectory."""
         if self.device.type != "cuda" or self.world > 1 or self.backend != "native":
             return False
+        # the fused SyncBN exchange takes its epoch as a host-side kernel argument: a captured
+        # launch would replay a stale epoch and pass its flag waits at once (ADVICE r3), so an
+        # emulated (or any native xGMI) SyncBN group keeps eager launches
+        if isinstance(self.sync_group, comm.EmulatedGroup):
+            return False
         self._idx_buf = idx_example.clone()
         state = [self.flat.flat, self.optimizer.buf, self.record_norm_mean, self._rnm_valid]
         state += [t for t in self.model.buffers()]
