@@ -393,6 +393,14 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
 
 }  // namespace
 
+std::vector<torch::Tensor>& side_stash();
+
+// a split-K slab whose reduction was queued (splitk_defer_begin) stays alive until the side
+// stream is joined (side_stash), i.e. past its deferred reduction launch
+void keep_deferred_partial(const torch::Tensor& part) {
+  if (part.defined() && splitk_deferring(cur_stream())) side_stash().push_back(part);
+}
+
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                          int64_t splits, int64_t cfg, c10::optional<torch::Tensor> out, bool accumulate,
                          OptT in_scale, OptT in_shift) {
@@ -507,17 +515,20 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     check_hip(launch_wgrad1x1(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
                               dw.data_ptr<float>(), (int)splits, accumulate ? 1 : 0, cur_stream()),
               "conv_wgrad(1x1)");
+    keep_deferred_partial(part);
     return dw;
   }
   if (w3) {
     check_hip(launch_wgrad3x3(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
                               dw.data_ptr<float>(), (int)splits, accumulate ? 1 : 0, cur_stream()),
               "conv_wgrad(3x3)");
+    keep_deferred_partial(part);
     return dw;
   }
   check_hip(launch_conv_wgrad(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
                               dw.data_ptr<float>(), (int)cfg, (int)splits, accumulate ? 1 : 0, cur_stream(), isc, ish),
             "conv_wgrad");
+  keep_deferred_partial(part);
   return dw;
 }
 
@@ -1082,6 +1093,18 @@ bool dgrad_bnstat_enabled() {
   return on;
 }
 
+// SDX_SPLITK_MERGE=0 (or splitk_merge_set(False)): one split-K reduction launch per weight
+// gradient (round-3 behaviour)
+std::atomic<int>& splitk_merge_flag() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("SDX_SPLITK_MERGE");
+    return e == nullptr || atoi(e) != 0 ? 1 : 0;
+  }()};
+  return on;
+}
+bool splitk_merge_enabled() { return splitk_merge_flag().load(std::memory_order_relaxed) != 0; }
+int64_t splitk_merge_set(bool on) { return splitk_merge_flag().exchange(on ? 1 : 0); }
+
 // tensors read by side-stream wgrads, released after the join (no recordStream: blocks
 // return to the allocator in program order instead of behind side-stream events)
 std::vector<torch::Tensor>& side_stash() {
@@ -1108,6 +1131,9 @@ void side_wgrad(const torch::Tensor& dy, const torch::Tensor& x, int64_t R, int6
   side_stash().push_back(dy);
   side_stash().push_back(x);
   c10::hip::HIPStreamGuard guard(hs);
+  // the reduction into the parameter sink joins the block's one multi-tensor launch
+  // (block_bwd flushes it before returning, i.e. before the sinks are announced final)
+  if (splitk_merge_enabled() && !splitk_deferring(ss)) splitk_defer_begin(ss);
   conv_wgrad(dy, x, R, S, stride, pad, 0, -1, sink, true, c10::nullopt, c10::nullopt);
 }
 
@@ -1146,6 +1172,9 @@ std::vector<torch::Tensor> fold_gram(torch::Tensor a2, int64_t side) {
 void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const torch::Tensor& w3,
                      const torch::Tensor& coef, const torch::Tensor& sink, int64_t side,
                      const torch::Tensor* gram = nullptr, const torch::Tensor* Gpre = nullptr) {
+  // its own split-K reductions (G, S) are read right after by bnfold_wgrad: issue any queued
+  // sink reductions first and keep this call's undeferred
+  if (side != 0 && splitk_deferring(reinterpret_cast<hipStream_t>(side))) check_hip(splitk_flush(), "splitk_flush");
   const int64_t C3 = dz.size(3), K3 = a2.size(3);
   auto body = [&]() {
     auto opt = coef.options();
@@ -1365,6 +1394,14 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
                                      std::vector<torch::Tensor> prev, std::vector<torch::Tensor> fold_w) {
   const int nconv = bottleneck ? 3 : 2;
   const int nbn = nconv + (proj ? 1 : 0);
+  // the side-stream sink reductions queued by side_wgrad go out as one launch when the block
+  // is done (before the caller announces the sinks final); dropped if the block throws
+  struct DeferGuard {
+    bool ok = false;
+    ~DeferGuard() {
+      if (!ok) splitk_defer_cancel();
+    }
+  } defer_guard;
   TORCH_CHECK((int)wt.size() == nbn && (int)dw.size() == nbn && (int)bng.size() == 3 * nbn &&
                   (int)bnst.size() == 4 * nbn && saved.size() == 8,
               "block_bwd: argument counts");
@@ -1561,6 +1598,8 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   } else {
     dx = last_dgrad(c10::nullopt, dout, out);
   }
+  check_hip(splitk_flush(), "splitk_flush");
+  defer_guard.ok = true;
   return {dx, prev_slab};
 }
 
@@ -1652,6 +1691,8 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("inv_b") = pybind11::none(), pybind11::arg("sink_ga") = pybind11::none(),
         pybind11::arg("sink_ba") = pybind11::none(), pybind11::arg("sink_gb") = pybind11::none(),
         pybind11::arg("sink_bb") = pybind11::none());
+  m.def("splitk_merge_set", &splitk_merge_set,
+        "merge a residual block's side-stream split-K reductions into one launch (returns the previous setting)");
   m.def("side_stash_release", &side_stash_release, "drop the tensors kept alive for side-stream wgrads (after join)");
   m.def("conv_dgrad_bnstat", &conv_dgrad_bnstat,
         "dgrad + fused BN-backward statistics of dx (slab [rows][2|3][C] for bn_bwd_coef_slab)",

@@ -117,6 +117,13 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
                              const float* in_shift = nullptr);
 // dW (+)= Σ_split partial[split] (fp32 [splits][n4*4]), deterministic order
 hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float* dw, int accumulate, hipStream_t s);
+// Deferral of the split-K reductions launched on stream s (this host thread): they are queued
+// until splitk_flush(), which issues them as one multi-tensor launch on s. The caller keeps
+// the partial slabs alive until then and must not read the queued dW before the flush.
+void splitk_defer_begin(hipStream_t s);
+bool splitk_deferring(hipStream_t s);
+hipError_t splitk_flush();
+void splitk_defer_cancel();   // drop the queue (error paths)
 // Tap-reuse 3x3 wgrad (wgrad3x3.hip): stride 1, pad 1, W in {4,8,16,32}, C,K % 64 == 0.
 // partial: fp32 [splits][K][9C] (unused when splits == 1 and !accumulate)
 bool wgrad3x3_supported(const ConvGeom& g);

@@ -1954,7 +1954,108 @@ hipError_t launch_conv_wgrad(const ConvGeom& g, const void* dy, const void* x, f
   return launch_splitk_reduce(partial, p.splits, (long)p.M * p.Ncol / 4, dw, accumulate, s);
 }
 
+// Deferred split-K reductions (SplitkDefer, launchers.h): while a stream is registered, the
+// reductions launched on it are queued and later issued as ONE multi-tensor launch
+// (splitk_flush), block b of which serves job j = the first with b < tiles_end[j] — a
+// residual block's 3-4 weight gradients become one reduction launch instead of 3-4.
+namespace {
+constexpr int kMaxSplitkJobs = 16;
+struct SplitkJobs {
+  const float* part[kMaxSplitkJobs];
+  float* dw[kMaxSplitkJobs];
+  long n4[kMaxSplitkJobs];
+  int splits[kMaxSplitkJobs];
+  int acc[kMaxSplitkJobs];
+  int tiles_end[kMaxSplitkJobs];
+  int n;
+};
+thread_local hipStream_t g_defer_stream = nullptr;
+thread_local SplitkJobs g_jobs{};
+
+__global__ __launch_bounds__(256) void splitk_reduce_multi_kernel(SplitkJobs jobs) {
+  int j = 0;
+  while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.tiles_end[j]) ++j;
+  const int b = blockIdx.x - (j ? jobs.tiles_end[j - 1] : 0);
+  __shared__ float4 red[4][64];
+  const float* __restrict__ part = jobs.part[j];
+  const long n4 = jobs.n4[j];
+  const int splits = jobs.splits[j];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long e = (long)b * 64 + tx;
+  const float4* P = reinterpret_cast<const float4*>(part);
+  float4 a[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n4) {
+    int k = ty;
+    for (; k + 12 < splits; k += 16) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = P[(size_t)(k + 4 * q) * n4 + e];
+        a[q].x += v.x; a[q].y += v.y; a[q].z += v.z; a[q].w += v.w;
+      }
+    }
+    for (; k < splits; k += 4) {
+      const float4 v = P[(size_t)k * n4 + e];
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
+  }
+  float4 sm = a[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q) { sm.x += a[q].x; sm.y += a[q].y; sm.z += a[q].z; sm.w += a[q].w; }
+  red[ty][tx] = sm;
+  __syncthreads();
+  if (ty == 0 && e < n4) {
+    float4* out = reinterpret_cast<float4*>(jobs.dw[j]);
+    float4 t = jobs.acc[j] ? out[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { t.x += red[q][tx].x; t.y += red[q][tx].y; t.z += red[q][tx].z; t.w += red[q][tx].w; }
+    out[e] = t;
+  }
+}
+}  // namespace
+
+void splitk_defer_begin(hipStream_t s) {
+  g_defer_stream = s;
+  g_jobs.n = 0;
+}
+
+bool splitk_deferring(hipStream_t s) { return g_defer_stream != nullptr && s == g_defer_stream; }
+
+void splitk_defer_cancel() {
+  g_defer_stream = nullptr;
+  g_jobs.n = 0;
+}
+
+hipError_t splitk_flush() {
+  hipStream_t s = g_defer_stream;
+  g_defer_stream = nullptr;
+  if (g_jobs.n == 0) return hipSuccess;
+  const int grid = g_jobs.tiles_end[g_jobs.n - 1];
+  hipLaunchKernelGGL(splitk_reduce_multi_kernel, dim3(grid), dim3(256), 0, s, g_jobs);
+  g_jobs.n = 0;
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float* dw, int accumulate, hipStream_t s) {
+  if (splitk_deferring(s)) {
+    if (g_jobs.n == kMaxSplitkJobs) {
+      // queue full: issue what is queued and keep deferring
+      hipStream_t keep = g_defer_stream;
+      const hipError_t e = splitk_flush();
+      if (e != hipSuccess) return e;
+      splitk_defer_begin(keep);
+    }
+    const int i = g_jobs.n++;
+    g_jobs.part[i] = partial;
+    g_jobs.dw[i] = dw;
+    g_jobs.n4[i] = n4;
+    g_jobs.splits[i] = splits;
+    g_jobs.acc[i] = accumulate;
+    g_jobs.tiles_end[i] = (i ? g_jobs.tiles_end[i - 1] : 0) + (int)((n4 + 63) / 64);
+    return hipSuccess;
+  }
   const long grid = (n4 + 63) / 64;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, partial, splits, n4, dw, accumulate);
   SDX_LAUNCH_CHECK();

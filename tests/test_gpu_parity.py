@@ -519,3 +519,32 @@ def test_teacher_forced_trajectory_gradients(gpu):
     assert mn <= 1.2 * mc + 0.02, (mn, mc)
     for lt_, ln_, _ in rows:
         assert abs(ln_ - lt_) <= 2e-3 * abs(lt_), rows
+
+
+def test_merged_splitk_reductions_bit_identical(gpu):
+    """The side-stream split-K reductions of a residual block merged into ONE multi-tensor
+    launch (splitk_merge_set, the default) give every parameter gradient bit for bit as one
+    reduction launch per weight gradient: same per-element summation order. A repeat of the
+    unmerged step first pins that the step itself is deterministic (the control)."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner, to_nhwc_input
+    from simclr_pytorch_distributed_amd.ops import _ext
+    from simclr_pytorch_distributed_amd.optim.flat import FlatParams
+    m = _ext.require()
+    nat_m, _ = _models(gpu, "resnet50")
+    flat = FlatParams(nat_m)
+    runner = ModelRunner(nat_m, "native", master=flat.flat)
+    x = to_nhwc_input(_images(gpu, 128, seed=4))
+    G = torch.randn(128, 128, generator=torch.Generator().manual_seed(6)).to(gpu)
+    grads = []
+    prev = m.splitk_merge_set(False)
+    try:
+        for merge in (False, False, True):
+            m.splitk_merge_set(merge)
+            flat.zero_grad()
+            (runner.forward(x) * G).sum().backward()
+            torch.cuda.synchronize()
+            grads.append(flat.grad.detach().clone())
+    finally:
+        m.splitk_merge_set(bool(prev))
+    assert torch.equal(grads[0], grads[1]), "unmerged step is not deterministic"
+    assert torch.equal(grads[0], grads[2])
