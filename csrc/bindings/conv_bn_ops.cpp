@@ -302,7 +302,18 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
               "conv_dgrad");
     return dx;
   }
-  // sub-pixel classes: each gets the taps r ≡ ph+pad, s ≡ pw+pad (mod stride)
+  // sub-pixel classes: each gets the taps r ≡ ph+pad, s ≡ pw+pad (mod stride); by default all
+  // of them in one launch (SDX_DGRAD_MERGE=0: one launch per class)
+  static const bool merge = [] {
+    const char* e = getenv("SDX_DGRAD_MERGE");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (merge && stride == 2) {
+    check_hip(launch_conv_dgrad_merged(g, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg, cur_stream(),
+                                       amask, bs, add ? (int)addend_sub : 0),
+              "conv_dgrad(merged classes)");
+    return dx;
+  }
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) {
       // each class reads its taps straight from the full Wt (no per-class weight copy; a
@@ -393,7 +404,12 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
 
 }  // namespace
 
-std::vector<torch::Tensor>& side_stash();
+// tensors read by side-stream wgrads, released after the join (no recordStream: blocks
+// return to the allocator in program order instead of behind side-stream events)
+std::vector<torch::Tensor>& side_stash() {
+  static std::vector<torch::Tensor> v;
+  return v;
+}
 
 // a split-K slab whose reduction was queued (splitk_defer_begin) stays alive until the side
 // stream is joined (side_stash), i.e. past its deferred reduction launch
@@ -1107,10 +1123,6 @@ int64_t splitk_merge_set(bool on) { return splitk_merge_flag().exchange(on ? 1 :
 
 // tensors read by side-stream wgrads, released after the join (no recordStream: blocks
 // return to the allocator in program order instead of behind side-stream events)
-std::vector<torch::Tensor>& side_stash() {
-  static std::vector<torch::Tensor> v;
-  return v;
-}
 
 void side_stash_release() { side_stash().clear(); }
 

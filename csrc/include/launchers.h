@@ -105,6 +105,11 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                    const BnBwdStat* bstat = nullptr, int addend_sub = 0,
                                    const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);
+// every sub-pixel class of a strided dgrad (stride 2) in ONE launch; bstat->row0 = the first
+// class's slab row (the classes' rows follow in the kernel's class order)
+hipError_t launch_conv_dgrad_merged(const ConvGeom& g, const void* dy, const void* wt, void* dx, const void* addend,
+                                    int cfg, hipStream_t s, const void* addend_mask = nullptr,
+                                    const BnBwdStat* bstat = nullptr, int addend_sub = 0);
 // in-kernel statistics reduction plan for an M x Ncol GEMM of tile config cfg
 int stat_fuse_groups(int m_tiles);
 int stat_fuse_counters(int m_tiles, int n_tiles);

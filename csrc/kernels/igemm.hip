@@ -135,6 +135,14 @@ struct IgemmParams {
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
   int ph, pw, Hc, Wc, r0, s0, nr, ns;
+  // DGRAD, ncls > 1: all stride² sub-pixel classes in ONE launch. Block tiles are class-major
+  // (class c owns tiles [cls[c-1].tile_end, cls[c].tile_end)); each block loads its class's
+  // fields over the per-class ones above (M, Kdim, b_t0, m_tiles, bs.row0 included)
+  struct Cls {
+    int ph, pw, Hc, Wc, r0, s0, nr, ns, M, Kdim, b_t0, m_tiles, row0, tile_end;
+  };
+  int ncls;
+  Cls cls[4];
   FastDiv div_pq, div_q;   // WGRAD pixel decode
 };
 
@@ -385,7 +393,11 @@ constexpr int igemm_min_waves() {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR, bool ONE>
-__global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN, VAR>())) void igemm_kernel(IgemmParams p) {
+__global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN, VAR>())) void igemm_kernel(
+    IgemmParams p_in) {
+  // a block-local copy: a merged strided-dgrad launch overwrites its class's fields (uniform
+  // values: SROA keeps the untouched fields in the kernel arguments)
+  IgemmParams p = p_in;
   constexpr int NT = 64 * WM * WN;   // threads per block (4 or 8 waves)
   using T = Tile<MODE, BM, BN, NT>;
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
@@ -443,6 +455,17 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     const int nt_all = p.m_tiles * p.n_tiles;
     if (p.worder) { tile = lin % nt_all; split = lin / nt_all; }
     else { split = lin % p.splits; tile = lin / p.splits; }
+  }
+  if constexpr (MODE == MODE_DGRAD) {
+    if (p_in.ncls > 1) {
+      int cid = 0;
+      while (cid + 1 < p_in.ncls && tile >= p_in.cls[cid].tile_end) ++cid;
+      if (cid > 0) tile -= p_in.cls[cid - 1].tile_end;
+      const IgemmParams::Cls& cd = p_in.cls[cid];
+      p.ph = cd.ph; p.pw = cd.pw; p.Hc = cd.Hc; p.Wc = cd.Wc; p.r0 = cd.r0; p.s0 = cd.s0;
+      p.nr = cd.nr; p.ns = cd.ns; p.M = cd.M; p.Kdim = cd.Kdim; p.b_t0 = cd.b_t0;
+      p.m_tiles = cd.m_tiles; p.bs.row0 = cd.row0;
+    }
   }
   const int mt = tile / p.n_tiles, nt = tile % p.n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -1697,7 +1720,22 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   p.trace = igemm_trace_on();
   p.m_tiles = (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
-  const int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
+  int grid = p.m_tiles * p.n_tiles * (MODE == MODE_WGRAD ? p.splits : 1);
+  if (MODE == MODE_DGRAD && p.ncls > 1) {
+    // merged sub-pixel classes: class-major tiles, each class's BN-statistics slab rows after
+    // the previous classes' (as the per-class launches advanced bs.row0)
+    int end = 0, row = p.bs.row0;
+    for (int c = 0; c < p.ncls; ++c) {
+      IgemmParams::Cls& cd = p.cls[c];
+      cd.m_tiles = (cd.M + BM - 1) / BM;
+      cd.row0 = row;
+      row += cd.m_tiles;
+      end += cd.m_tiles * p.n_tiles;
+      cd.tile_end = end;
+    }
+    grid = end;
+    if (grid == 0) return hipSuccess;
+  }
   if (p.sf.cnt != nullptr &&
       (MODE == MODE_WGRAD || p.sf.group < 1 || p.sf.n_groups != (p.m_tiles + p.sf.group - 1) / p.sf.group))
     return hipErrorInvalidValue;   // the plan must match this tile config (stat_fuse_groups)
@@ -1894,6 +1932,65 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   p.b_ts = g.stride * g.K;
   p.a_elems = (long)g.N * g.P * g.Q * g.K;
   p.b_elems = (long)p.Ncol * p.b_row;
+  return launch_any<MODE_DGRAD>(p, cfg, s);
+}
+
+hipError_t launch_conv_dgrad_merged(const ConvGeom& g, const void* dy, const void* wt, void* dx, const void* addend,
+                                    int cfg, hipStream_t s, const void* addend_mask, const BnBwdStat* bstat,
+                                    int addend_sub) {
+  const int st = g.stride;
+  if (st < 2 || st * st > 4) return hipErrorInvalidValue;
+  IgemmParams p{};
+  p.addend_sub = addend_sub;
+  if (bstat != nullptr) p.bs = *bstat;
+  p.addend_mask = (const uint8_t*)addend_mask;
+  p.g = g;
+  p.a = (const uint16_t*)dy;
+  p.b = (const uint16_t*)wt;
+  p.out = dx;
+  p.addend = (const uint16_t*)addend;
+  p.Ncol = g.C;
+  p.b_row = g.R * g.S * g.K;
+  p.b_tr = st * g.S * g.K;
+  p.b_ts = st * g.K;
+  p.a_elems = (long)g.N * g.P * g.Q * g.K;
+  p.b_elems = (long)p.Ncol * p.b_row;
+  // classes with more taps first (longest blocks dispatched first)
+  int order[4], n = 0;
+  for (int ph = 0; ph < st; ++ph)
+    for (int pw = 0; pw < st; ++pw) order[n++] = ph * st + pw;
+  auto taps = [&](int id) {
+    int r0, nr, s0, ns, Hc, Wc;
+    conv_dgrad_class(g, id / st, id % st, &r0, &nr, &s0, &ns, &Hc, &Wc);
+    return nr * ns;
+  };
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && taps(order[j]) > taps(order[j - 1]); --j) std::swap(order[j], order[j - 1]);
+  int maxk = 0, maxm = 0, maxt = 0, nc = 0;
+  for (int i = 0; i < n; ++i) {
+    IgemmParams::Cls& cd = p.cls[nc];
+    cd.ph = order[i] / st;
+    cd.pw = order[i] % st;
+    conv_dgrad_class(g, cd.ph, cd.pw, &cd.r0, &cd.nr, &cd.s0, &cd.ns, &cd.Hc, &cd.Wc);
+    cd.M = g.N * cd.Hc * cd.Wc;
+    if (cd.M == 0) continue;
+    cd.Kdim = cd.nr * cd.ns * g.K;
+    cd.b_t0 = (cd.r0 * g.S + cd.s0) * g.K;
+    maxk = cd.Kdim > maxk ? cd.Kdim : maxk;
+    maxm = cd.M > maxm ? cd.M : maxm;
+    maxt = cd.nr * cd.ns > maxt ? cd.nr * cd.ns : maxt;
+    ++nc;
+  }
+  if (nc == 0) return hipSuccess;
+  p.ncls = nc;
+  // launch-level choices (main loop, single-stage form) see the largest class; the per-class
+  // fields below are the first class's (every block overwrites them with its own)
+  const IgemmParams::Cls& c0 = p.cls[0];
+  p.ph = c0.ph; p.pw = c0.pw; p.Hc = c0.Hc; p.Wc = c0.Wc; p.r0 = c0.r0; p.s0 = c0.s0;
+  p.nr = c0.nr; p.ns = c0.ns; p.b_t0 = c0.b_t0;
+  p.M = maxm;
+  p.Kdim = maxk;
+  (void)maxt;
   return launch_any<MODE_DGRAD>(p, cfg, s);
 }
 
