@@ -185,8 +185,12 @@ def test_trajectory_tracks_fp32(gpu):
     torch bf16 autocast as the control. Single steps of this trajectory are chaotic for
     ANY bf16 path (measured per-step gaps to fp32 up to 3 % native and 1.6 % autocast at
     lr 0.05, batch 128: tools/trajectory_probe.py), so the comparison is on 10-step window
-    means: native within max(2.5 %, 2x the autocast gap) of fp32 in every window, and the
-    fp32 and native losses must both fall by 3 % (no collapsed run passes)."""
+    means: native within max(2.5 %, 2x the autocast gap, 2x the fp32 reference's own
+    run-to-run gap) of fp32 in every window, and the fp32 and native losses must both fall by
+    3 % (no collapsed run passes). The fp32 torch path is not deterministic on ROCm (MIOpen):
+    its window-1 mean moved 35.7 -> 36.7 across five runs of the same native trajectory
+    (round 4), so a second fp32 replica from the same init runs alongside and its gap to the
+    first is part of the bar."""
     from simclr_pytorch_distributed_amd.data.augment import AugConfig, gpu_augment, nhwc8_to_nchw
     from simclr_pytorch_distributed_amd.data.datasets import build_dataset
     from simclr_pytorch_distributed_amd.losses.supcon import DistributedContrastiveLoss
@@ -194,17 +198,18 @@ def test_trajectory_tracks_fp32(gpu):
     from simclr_pytorch_distributed_amd.optim.flat import FlatParams, FusedSGD
     nat_m, ref_m = _models(gpu, "resnet18")
     ctl_m = _autocast_copy(gpu, ref_m)
+    ref2_m = _models(gpu, "resnet18")[1]                  # same init (seed 0) as ref_m
     flat = FlatParams(nat_m)
     runner = ModelRunner(nat_m, "native", master=flat.flat)
     lr0, B = 0.05, 128
     opt_n = FusedSGD(flat, lr=lr0, momentum=0.9, weight_decay=1e-4)
-    opts = [torch.optim.SGD(m.parameters(), lr=lr0, momentum=0.9, weight_decay=1e-4) for m in (ref_m, ctl_m)]
+    opts = [torch.optim.SGD(m.parameters(), lr=lr0, momentum=0.9, weight_decay=1e-4) for m in (ref_m, ctl_m, ref2_m)]
     crit_n = DistributedContrastiveLoss("SimCLR", 0.5, backend="native")
     crit_t = DistributedContrastiveLoss("SimCLR", 0.5, backend="torch")
     ds = build_dataset("cifar10", None, True, True, 4096, 32, 0)
     data = torch.from_numpy(ds.images).to(gpu)
     aug = AugConfig.simclr(32, (0.4914, 0.4822, 0.4465), (0.2023, 0.1994, 0.2010))
-    L = {"n": [], "t": [], "c": []}
+    L = {"n": [], "t": [], "c": [], "t2": []}
     for step in range(50):
         lr = lr0 * min(1.0, (step + 1) / 10)
         for o in opts:
@@ -227,18 +232,22 @@ def test_trajectory_tracks_fp32(gpu):
             lc = crit_t(ctl_m(vt).float())
         lc.backward()
         opts[1].step()
-        for k, l in (("n", ln), ("t", lt), ("c", lc)):
+        opts[2].zero_grad()
+        lt2 = crit_t(ref2_m(vt))
+        lt2.backward()
+        opts[2].step()
+        for k, l in (("n", ln), ("t", lt), ("c", lc), ("t2", lt2)):
             L[k].append(float(l.detach()))
     torch.cuda.synchronize()
     W = {k: [sum(v[w:w + 10]) / 10 for w in range(0, 50, 10)] for k, v in L.items()}
     print("window means native", [round(v, 3) for v in W["n"]], "fp32", [round(v, 3) for v in W["t"]],
-          "autocast", [round(v, 3) for v in W["c"]])
-    mn, mt, mc = W["n"], W["t"], W["c"]
+          "autocast", [round(v, 3) for v in W["c"]], "fp32 replica", [round(v, 3) for v in W["t2"]])
+    mn, mt, mc, mt2 = W["n"], W["t"], W["c"], W["t2"]
     assert mt[0] - min(mt[-2:]) > 0.03 * mt[0], ("fp32 trajectory did not fall", mt)
     assert mn[0] - min(mn[-2:]) > 0.03 * mn[0], ("native trajectory did not fall", mn)
     for w in range(5):
-        tol = max(0.025 * mt[w], 2 * abs(mc[w] - mt[w]))
-        assert abs(mn[w] - mt[w]) <= tol, (w, mn[w], mt[w], mc[w])
+        tol = max(0.025 * mt[w], 2 * abs(mc[w] - mt[w]), 2 * abs(mt2[w] - mt[w]))
+        assert abs(mn[w] - mt[w]) <= tol, (w, mn[w], mt[w], mc[w], mt2[w])
 
 
 def test_bn3_fold_forward_matches(gpu, monkeypatch):
