@@ -454,14 +454,32 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     const char* e = getenv("SDX_WGRAD_WIDE64");
     return e == nullptr || atoi(e) != 0;
   }();
+  // The stage-1 weight gradients (the most pixels) are the last work of the backward: when
+  // they run, the main stream has (almost) nothing left, so the half-chip block target that
+  // keeps the side stream off the critical-path kernels only leaves CUs idle in the step's
+  // tail (profiles: a 390 us gap before the SGD at 256 images/GPU). GEMMs with at least
+  // SDX_W3_TAIL_PIX pixels (2^18 = stage 1 at 128 and 256 images/GPU) get
+  // SDX_W3_TAIL_BLOCKS (default 256) blocks. Default 0 (off): the gap shrinks to 180 us but
+  // the wider stage-1 wgrads slow the concurrent stage-1 dgrads more, 12.43 vs 12.37 ms
+  // (512 blocks: 12.52; same-box A/B, profiles/tail_ab_r4.txt)
+  static const int64_t tail_pix = [] {
+    const char* e = getenv("SDX_W3_TAIL_PIX");
+    return e ? atoll(e) : 0LL;
+  }();
+  static const int64_t tail_blocks = [] {
+    const char* e = getenv("SDX_W3_TAIL_BLOCKS");
+    return e ? atoll(e) : 256LL;
+  }();
+  const bool tail = tail_pix > 0 && Kd >= tail_pix;
   if (w1) {
     // as for the 3x3 kernel: SDX_W3_BLOCKS (128) 8-wave blocks, >= 8 steps each
     const int64_t steps = wgrad1x1_steps(g);
     if (splits <= 0) {
-      static const int64_t target = [] {
+      static const int64_t target0 = [] {
         const char* e = getenv("SDX_W3_BLOCKS");
         return e ? atoll(e) : 128LL;
       }();
+      const int64_t target = tail ? tail_blocks : target0;
       splits = std::max<int64_t>(1, target / wgrad1x1_tiles(g));
       splits = std::min(splits, std::max<int64_t>(1, steps / 8));
     }
@@ -475,10 +493,11 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
       // so the critical-path kernels (128-VGPR dgrads, the BN reductions) cannot co-reside on
       // its CU. 128 blocks leave half the CUs to the main stream: step 13.71 -> 13.34 ms at
       // 256 images/GPU, 8.48 -> 8.20 ms at 128 (profiles/wgrad3x3_r2.txt)
-      static const int64_t target = [] {
+      static const int64_t target0 = [] {
         const char* e = getenv("SDX_W3_BLOCKS");
         return e ? atoll(e) : 128LL;
       }();
+      const int64_t target = tail ? tail_blocks : target0;
       const int64_t tiles = wgrad3x3_tiles(g), steps = wgrad3x3_steps(g);
       splits = std::max<int64_t>(1, target / tiles);
       splits = std::min(splits, std::max<int64_t>(1, steps / 8));

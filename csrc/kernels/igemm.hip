@@ -135,9 +135,10 @@ struct IgemmParams {
   int m_tiles, n_tiles, splits, k_per_split;
   // DGRAD sub-pixel class: output rows h = st·h' + ph, taps r = r0 + st·ir (ir < nr)
   int ph, pw, Hc, Wc, r0, s0, nr, ns;
-  // DGRAD, ncls > 1: all stride² sub-pixel classes in ONE launch. Block tiles are class-major
-  // (class c owns tiles [cls[c-1].tile_end, cls[c].tile_end)); each block loads its class's
-  // fields over the per-class ones above (M, Kdim, b_t0, m_tiles, bs.row0 included)
+  // DGRAD, ncls > 1: all stride² sub-pixel classes in ONE launch. Block tiles interleave the
+  // classes (tile t -> class t % ncls, its tile t / ncls < cls.tile_end = that class's tile
+  // count); each block loads its class's fields over the per-class ones above (M, Kdim, b_t0,
+  // m_tiles, bs.row0 included)
   struct Cls {
     int ph, pw, Hc, Wc, r0, s0, nr, ns, M, Kdim, b_t0, m_tiles, row0, tile_end;
   };
@@ -458,10 +459,13 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   }
   if constexpr (MODE == MODE_DGRAD) {
     if (p_in.ncls > 1) {
-      int cid = 0;
-      while (cid + 1 < p_in.ncls && tile >= p_in.cls[cid].tile_end) ++cid;
-      if (cid > 0) tile -= p_in.cls[cid - 1].tile_end;
+      // classes interleaved tile by tile: the XCD-aware order gives every XCD an equal share
+      // of each class (class-major order put a stride-2 1x1 dgrad's only non-empty class on
+      // two XCDs: 2x slower)
+      const int cid = tile % p_in.ncls;
+      tile /= p_in.ncls;
       const IgemmParams::Cls& cd = p_in.cls[cid];
+      if (tile >= cd.tile_end) return;   // this class has fewer tiles than the largest
       p.ph = cd.ph; p.pw = cd.pw; p.Hc = cd.Hc; p.Wc = cd.Wc; p.r0 = cd.r0; p.s0 = cd.s0;
       p.nr = cd.nr; p.ns = cd.ns; p.M = cd.M; p.Kdim = cd.Kdim; p.b_t0 = cd.b_t0;
       p.m_tiles = cd.m_tiles; p.bs.row0 = cd.row0;
@@ -1724,16 +1728,16 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   if (MODE == MODE_DGRAD && p.ncls > 1) {
     // merged sub-pixel classes: class-major tiles, each class's BN-statistics slab rows after
     // the previous classes' (as the per-class launches advanced bs.row0)
-    int end = 0, row = p.bs.row0;
+    int most = 0, row = p.bs.row0;
     for (int c = 0; c < p.ncls; ++c) {
       IgemmParams::Cls& cd = p.cls[c];
       cd.m_tiles = (cd.M + BM - 1) / BM;
       cd.row0 = row;
       row += cd.m_tiles;
-      end += cd.m_tiles * p.n_tiles;
-      cd.tile_end = end;
+      cd.tile_end = cd.m_tiles * p.n_tiles;
+      most = cd.tile_end > most ? cd.tile_end : most;
     }
-    grid = end;
+    grid = most * p.ncls;
     if (grid == 0) return hipSuccess;
   }
   if (p.sf.cnt != nullptr &&
