@@ -304,11 +304,14 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   }
   // sub-pixel classes: each gets the taps r ≡ ph+pad, s ≡ pw+pad (mod stride); by default all
   // of them in one launch (SDX_DGRAD_MERGE=0: one launch per class)
-  static const bool merge = [] {
+  // SDX_DGRAD_MERGE: 0 one launch per class, 1 merged for every strided dgrad, 2 merged for
+  // strided 3x3 only (default: a strided 1x1 has one non-empty class, whose launch is faster
+  // on its own — profiles/dgrad_merge_r4.txt)
+  static const int merge = [] {
     const char* e = getenv("SDX_DGRAD_MERGE");
-    return e == nullptr || atoi(e) != 0;
+    return e == nullptr ? 2 : atoi(e);
   }();
-  if (merge && stride == 2) {
+  if (stride == 2 && (merge == 1 || (merge == 2 && g.R > 1))) {
     check_hip(launch_conv_dgrad_merged(g, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg, cur_stream(),
                                        amask, bs, add ? (int)addend_sub : 0),
               "conv_dgrad(merged classes)");
