@@ -105,7 +105,12 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
             raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
         return obj, True
 
-    tasks = [(s, kflags) for s in kern] + [(s, bflags) for s in bind]
+    # igemm.hip: MFMA accumulators in arch VGPRs. Its 4-wave 64x128 wave tiles (cfgs 7/8) hold
+    # 128 fp32 accumulators per lane; with the default AGPR heuristics hipcc copied them through
+    # a temporary around every MFMA (~600 v_accvgpr moves per kernel); the VGPR form needs 256
+    # VGPRs + 20 AGPRs and no copies. Every other instantiation compiles to the same code.
+    per_file = {"igemm.hip": ["-mllvm", "--amdgpu-mfma-vgpr-form"]}
+    tasks = [(s, kflags + per_file.get(os.path.basename(s), [])) for s in kern] + [(s, bflags) for s in bind]
     n = jobs or min(8, os.cpu_count() or 4)
     with ThreadPoolExecutor(max_workers=n) as ex:
         results = list(ex.map(lambda t: job(*t), tasks))

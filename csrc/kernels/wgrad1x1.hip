@@ -16,9 +16,11 @@
 // fp32 partial slab per K-split, reduced deterministically by igemm.hip's split-K reduction.
 //
 // Shapes: K % 128 == 0, C % BN == 0 (BN = 256, or 128 when C is not a multiple of 256),
-// N·H·W % 32 == 0 — layers 2-4 of the CIFAR/ImageNet ResNet bottlenecks (reference
-// networks/resnet_big.py:44-49, conv1/conv3 of each Bottleneck). The layer-1 1x1 wgrads
-// (64 channels on one side) are HBM-bound and stay on the generic kernel.
+// N·P·Q % 32 == 0 — layers 2-4 of the CIFAR/ImageNet ResNet bottlenecks (reference
+// networks/resnet_big.py:44-49, conv1/conv3 of each Bottleneck), and the strided projection
+// shortcuts (:50-55) when a step is whole output rows (pipelined kernel: each x chunk reads
+// its pixel at base + step·const). The layer-1 1x1 wgrads (64 channels on one side) are
+// HBM-bound and stay on the generic kernel.
 #include <type_traits>
 
 #include "common.h"
@@ -54,7 +56,11 @@ struct W1Params {
   const uint16_t* x;    // [P][C]
   float* part;          // [splits][K][C]
   int K, C;
-  int steps_total;      // P / 32
+  int steps_total;      // dy pixels / 32
+  // x pixel of dy pixel j of a step (pipelined kernel): stride 1: j; stride st (H = st·P,
+  // W = st·Q, Q | 32): st·(W·(j / Q) + j % Q). x step stride in elements (32·C at stride 1)
+  int xst, xq, xw;
+  int x_step;
   int steps_per_split;
   int k_tiles, c_tiles, splits;
 };
@@ -256,11 +262,13 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   const int a_off = (tid / A_CPR) * p.K + k0 + (tid % A_CPR) * 8;
   const int a_dst = w1_off<W1_BM>(tid / A_CPR, tid % A_CPR);
   const int e1 = tid, e2 = tid + W1_NT;   // x chunk indices of chunks 1, 2
-  const int x_off1 = (e1 / B_CPR) * p.C + c0 + (e1 % B_CPR) * 8;
-  const int x_off2 = (e2 / B_CPR) * p.C + c0 + (e2 % B_CPR) * 8;
+  // x pixel of step pixel j (a strided 1x1 reads every st-th pixel of every st-th row)
+  auto xpix = [&](int j) { return p.xst * (p.xw * (j / p.xq) + j % p.xq); };
+  const int x_off1 = xpix(e1 / B_CPR) * p.C + c0 + (e1 % B_CPR) * 8;
+  const int x_off2 = xpix(e2 / B_CPR) * p.C + c0 + (e2 % B_CPR) * 8;
   const int x_dst1 = A_BYTES + w1_off<BN>(e1 / B_CPR, e1 % B_CPR);
   const int x_dst2 = A_BYTES + w1_off<BN>(e2 / B_CPR, e2 % B_CPR);
-  const int sA = 32 * p.K, sB = 32 * p.C;
+  const int sA = 32 * p.K, sB = p.x_step;
   w1_gptr zp = (w1_gptr)w1_zero16;
   asm volatile("" : "+s"(zp));
   const w1_gptr gdy = (w1_gptr)p.dy, gx = (w1_gptr)p.x;
@@ -408,20 +416,30 @@ bool w1_pipe_enabled(const ConvGeom& g) {
     const char* e = getenv("SDX_W1_PIPE");
     return e == nullptr || atoi(e) != 0;
   }();
-  const long P = (long)g.N * g.H * g.W;   // 32-bit element offsets
-  return on && P * g.K < (1L << 31) && P * g.C < (1L << 31);
+  // 32-bit element offsets: dy (output pixels) and x (input pixels)
+  return on && (long)g.N * g.P * g.Q * g.K < (1L << 31) && (long)g.N * g.H * g.W * g.C < (1L << 31);
 }
 
 }  // namespace
 
+// stride 1 (any image size), or a strided 1x1 (projection shortcut, reference
+// networks/resnet_big.py:50-55) on the pipelined kernel when the input is exactly st x the
+// output and a 32-pixel step is whole output rows (Q | 32: the x source of a step pixel is
+// then base + step·const)
 bool wgrad1x1_supported(const ConvGeom& g) {
-  return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0 && g.P == g.H && g.Q == g.W && g.K % W1_BM == 0 &&
-         g.C % 128 == 0 && ((long)g.N * g.H * g.W) % 32 == 0;
+  static const bool strided_on = [] {   // SDX_W1_STRIDED=0: strided shortcuts on the generic kernel
+    const char* e = getenv("SDX_W1_STRIDED");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const bool strided_ok = strided_on && g.stride > 1 && g.H == g.stride * g.P && g.W == g.stride * g.Q && 32 % g.Q == 0 &&
+                          w1_pipe_enabled(g);
+  return g.R == 1 && g.S == 1 && g.pad == 0 && (g.stride == 1 ? (g.P == g.H && g.Q == g.W) : strided_ok) &&
+         g.K % W1_BM == 0 && g.C % 128 == 0 && ((long)g.N * g.P * g.Q) % 32 == 0;
 }
 
 int wgrad1x1_tiles(const ConvGeom& g) { return (g.K / W1_BM) * (g.C / wgrad1x1_bn(g)); }
 
-int wgrad1x1_steps(const ConvGeom& g) { return (int)((long)g.N * g.H * g.W / 32); }
+int wgrad1x1_steps(const ConvGeom& g) { return (int)((long)g.N * g.P * g.Q / 32); }
 
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s) {
@@ -432,6 +450,13 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   p.K = g.K;
   p.C = g.C;
   p.steps_total = wgrad1x1_steps(g);
+  if (g.stride == 1) {
+    p.xst = 1, p.xq = 32, p.xw = 32;   // xpix(j) = j
+    p.x_step = 32 * g.C;
+  } else {
+    p.xst = g.stride, p.xq = g.Q, p.xw = g.W;
+    p.x_step = g.stride * g.W * (32 / g.Q) * g.C;
+  }
   p.steps_per_split = (p.steps_total + splits - 1) / splits;
   p.splits = (p.steps_total + p.steps_per_split - 1) / p.steps_per_split;
   const int bn = wgrad1x1_bn(g);
@@ -441,7 +466,7 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   if (!direct && partial == nullptr) return hipErrorInvalidValue;
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W1_NT);
-  if (w1_pipe_enabled(g)) {
+  if (w1_pipe_enabled(g)) {   // (a strided shape is supported only when it is)
     if (bn == 256) hipLaunchKernelGGL(wgrad1x1_pipe_kernel<256>, grid, block, 0, s, p);
     else hipLaunchKernelGGL(wgrad1x1_pipe_kernel<128>, grid, block, 0, s, p);
   } else if (bn == 256) {

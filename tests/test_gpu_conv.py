@@ -135,6 +135,30 @@ def test_wgrad1x1_stream(gpu, shape, splits):
         assert torch.equal(m.conv_wgrad(dyh, xh, 1, 1, 1, 0, 0, -1), dw)
 
 
+@pytest.mark.parametrize("shape", [(4, 32, 256, 512), (8, 16, 512, 256), (16, 8, 256, 128), (4, 8, 128, 256)])
+@pytest.mark.parametrize("splits", [1, 3, 0])
+def test_wgrad1x1_strided(gpu, shape, splits):
+    """Stride-2 1x1 wgrad (projection shortcut, reference networks/resnet_big.py:50-55) on the
+    pipelined 1x1 kernel (cfg 10): output widths 16 / 8 / 4 (a 32-pixel step is 2 / 4 / 8
+    output rows, crossing images at 4 and 8), vs fp32 torch; direct, split-K, auto, sink."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, C, K = shape
+    x, w = _mk(N, H, H, C, K, 1)
+    wf = w.float().requires_grad_(True)
+    out = F.conv2d(x.float(), wf, stride=2)
+    dy = torch.randn_like(out).bfloat16()
+    (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
+    dyh, xh = dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    dw = m.conv_wgrad(dyh, xh, 1, 1, 2, 0, splits, 10)
+    assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
+    sink = torch.full((K, 1, 1, C), 0.25, device=gpu)
+    m.conv_wgrad(dyh, xh, 1, 1, 2, 0, splits, 10, sink, True)
+    assert _rel(sink - 0.25, dw.float()) < 1e-5
+    if splits == 0:
+        assert torch.equal(m.conv_wgrad(dyh, xh, 1, 1, 2, 0, 0, -1), dw)
+
+
 def test_conv_large_m(gpu):
     """Layer-1 scale (M = 512·32·32) against torch bf16 conv."""
     from simclr_pytorch_distributed_amd.ops import _ext

@@ -80,11 +80,24 @@ def main():
                       lambda: torch.ops.aten.convolution_backward(dyc, xc, wc, None, [st, st], [pad, pad], [1, 1],
                                                                   False, [0, 0], 1, [False, True, False])),
         }
+        if R == 1 and st > 1:
+            # what the step runs for a strided 1x1 shortcut (block_bwd sub_addend): the data
+            # gradient lives on the stride-s subgrid only, so it is a stride-1 1x1 dgrad on the
+            # P x Q grid that the block's final dgrad adds there (no zero sub-pixel classes)
+            runs["dgrad_c"] = (lambda: m.conv_dgrad(dy, wt, P, P, 1, 0, a.cfg), runs["dgrad"][1])
+        t_of = {}
         for ps, (nat, mio) in runs.items():
             if name == "stem" and ps == "dgrad":
                 continue
             tn = timeit(nat, a.iters)
-            tm = 0.0 if a.no_miopen or name == "stem" else timeit(mio, a.iters)
+            tm = 0.0 if a.no_miopen or name == "stem" or ps == "dgrad_c" else timeit(mio, a.iters)
+            if ps == "dgrad_c":
+                # replaces the full-grid dgrad row in the totals
+                tot["dgrad"][0] += (tn - t_of["dgrad"]) * cnt
+                print(f"{name:14s} {ps:6s} {N * P * P:8d} {C:5d} {K:5d} {tn:10.1f} {flops / tn / 1e6:7.1f} "
+                      f"{tm:10.1f} {flops / tm / 1e6 if tm else 0:7.1f}  x{cnt} (as run in the step)", flush=True)
+                continue
+            t_of[ps] = tn
             tot[ps][0] += tn * cnt
             tot[ps][1] += tm * cnt
             Mg = N * P * P if ps != "wgrad" else K
