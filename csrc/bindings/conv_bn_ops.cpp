@@ -441,7 +441,7 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     return e == nullptr || atoi(e) != 0;
   }();
   const bool w3 = (cfg == 9 || (cfg == -1 && w3_on && splits <= 0)) && !in_scale.has_value() && wgrad3x3_supported(g);
-  TORCH_CHECK(cfg != 9 || w3, "conv_wgrad: cfg 9 needs a stride-1 pad-1 3x3 conv with W in {4,8,16,32}, C,K % 64 == 0");
+  TORCH_CHECK(cfg != 9 || w3, "conv_wgrad: cfg 9 needs a pad-1 3x3 conv of stride 1 or 2 on square images with output width in {4,8,16,32}, C,K % 64 == 0");
   // cfg 10 = the stride-1 1x1 kernel (wgrad1x1.hip), auto-picked for every shape it supports
   // (SDX_WGRAD1=0: generic only)
   static const bool w1_on = [] {

@@ -129,7 +129,7 @@ void splitk_defer_begin(hipStream_t s);
 bool splitk_deferring(hipStream_t s);
 hipError_t splitk_flush();
 void splitk_defer_cancel();   // drop the queue (error paths)
-// Tap-reuse 3x3 wgrad (wgrad3x3.hip): stride 1, pad 1, W in {4,8,16,32}, C,K % 64 == 0.
+// Tap-reuse 3x3 wgrad (wgrad3x3.hip): stride 1 or 2, pad 1, output width in {4,8,16,32}, C,K % 64 == 0.
 // partial: fp32 [splits][K][9C] (unused when splits == 1 and !accumulate)
 bool wgrad3x3_supported(const ConvGeom& g);
 int wgrad3x3_tiles(const ConvGeom& g);

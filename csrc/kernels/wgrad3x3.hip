@@ -447,6 +447,192 @@ __global__ __launch_bounds__(W3P_NT, 1) void wgrad3x3_pipe_kernel(W3Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Stride-2 variant (the first 3x3 conv of layers 2-4, reference networks/resnet_big.py:45):
+//
+//   dW[k][r][s][c] = Σ dy[n][ho][wo][k] · x[n][2ho+r−1][2wo+s−1][c]
+//
+// Same block tile (64 output x 64 input channels x all 9 taps), same 32-pixel steps (RPS =
+// 32/Q whole output rows) and the same fragment images as wgrad3x3_kernel; only the x window
+// differs. Consecutive output pixels read every other input column, so each window row (tap
+// row r, output row i — input row 2ho+r−1) is stored DE-INTERLEAVED: an odd block
+// O[0..Q] = input columns −1, 1, ..., 2Q−1 (O[0] is the zero pad) and an even block
+// E[0..Q−1] = columns 0, 2, ..., 2Q−2. Tap s = 0 / 1 / 2 of output column wo then reads
+// O[wo] / E[wo] / O[wo+1]: consecutive pixels are consecutive LDS rows again, so the
+// swizzle stays conflict-free; the window row pitch PT keeps pixels 8 apart at a distance
+// ≡ 8 (mod 16) rows (Q = 8: PT = 24; Q = 4: two output rows, PT = 12). Per step: 256 dy
+// chunks + 3·RPS·2Q·8 = 1536 x chunks (every input column of 3·RPS input rows), 3.5 per
+// thread; a 2-deep register ring keeps VGPRs at the stride-1 kernel's level.
+template <int Q>
+struct W3S2Geom {
+  static constexpr int RPS = 32 / Q;
+  static constexpr int PT = Q >= 16 ? 2 * Q + 1 : Q == 8 ? 24 : 12;
+  static_assert(PT >= 2 * Q + 1, "window row");
+  static constexpr int XROWS = 3 * RPS * PT;
+  static constexpr int STAGE = W3_DY_BYTES + XROWS * W3_ROWB;
+  static constexpr int XCH = 3 * RPS * 2 * Q * 8;    // x chunks per step (1536)
+  static_assert(XCH == 1536, "loader layout");
+};
+
+template <int Q>
+__global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
+  using G = W3S2Geom<Q>;
+  constexpr int RPS = G::RPS, W = 2 * Q;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h4 = lane >> 4, c16 = lane & 15;
+  const int wm = wv >> 2, wn = wv & 3;
+
+  const int tiles = p.k_tiles * p.c_tiles;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lin % tiles, split = lin / tiles;
+  const int k0 = (tile / p.c_tiles) * 64, c0 = (tile % p.c_tiles) * 64;
+  const int s_begin = split * p.steps_per_split;
+  const int s_end = min(p.steps_total, s_begin + p.steps_per_split);
+
+  // zero pads O[0] of every window row in both buffers (never written by the loads)
+  for (int e = tid; e < 2 * 3 * RPS * 8; e += W3_NT) {
+    const int ch = e & 7, ri = (e >> 3) % (3 * RPS), buf = (e >> 3) / (3 * RPS);
+    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + W3_DY_BYTES + w3_off(ri * G::PT, ch)) =
+        make_uint4(0u, 0u, 0u, 0u);
+  }
+
+  // loader: chunk f = tid + 512u (u < 4, f < 1792): f < 256 a dy chunk (pixel f/8, channel
+  // chunk f%8), else x chunk e = f − 256: channel chunk e%8 of input column e/8 % 2Q of
+  // window row ri = e/(16Q) = (r, i). Output row Rg = step·RPS + i (global over images, H =
+  // 2P) reads input row 2Rg + r − 1: x element base + step·(2·RPS·W·C)
+  struct XChunk {
+    const uint16_t* base;   // element of step 0 (used only when valid)
+    int i, r, dst;
+  };
+  auto x_chunk = [&](int e) -> XChunk {
+    const int ch = e & 7, rest = e >> 3;
+    const int col = rest % W, ri = rest / W;
+    const int r = ri / RPS, i = ri % RPS;
+    const int lrow = ri * G::PT + ((col & 1) ? (col + 1) >> 1 : Q + 1 + (col >> 1));
+    return {p.x + ((long)(2 * i + r - 1) * W + col) * p.C + c0 + ch * 8, i, r, W3_DY_BYTES + w3_off(lrow, ch)};
+  };
+  const long x_step = 2L * RPS * W * p.C;
+  auto x_src = [&](const XChunk& xc, int step) -> const uint16_t* {
+    const int hi = 2 * ((step * RPS + xc.i) & (Q - 1)) + xc.r - 1;   // input row within the image
+    const bool ok = step < s_end && (unsigned)hi < (unsigned)W;
+    return ok ? xc.base + (long)step * x_step : w3_zero16;
+  };
+  const bool first_dy = tid < 256, last_x = tid < 256;
+  const XChunk xa = x_chunk(first_dy ? 0 : tid - 256), xb = x_chunk(tid + 256), xc_ = x_chunk(tid + 768),
+               xd = x_chunk(last_x ? tid + 1280 : 0);
+  const int dst_a = first_dy ? w3_off(tid >> 3, tid & 7) : xa.dst;
+  const uint16_t* dy_base = p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
+  // 2-step register ring of named uint4s (a struct of uint4 read through the lambdas ends up
+  // in scratch)
+  uint4 ra0, rb0, rc0, rd0, ra1, rb1, rc1, rd1;
+  auto load = [&](int step, uint4& a, uint4& b, uint4& c, uint4& d) {
+    a = *reinterpret_cast<const uint4*>(first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : w3_zero16)
+                                                 : x_src(xa, step));
+    b = *reinterpret_cast<const uint4*>(x_src(xb, step));
+    c = *reinterpret_cast<const uint4*>(x_src(xc_, step));
+    d = *reinterpret_cast<const uint4*>(last_x ? x_src(xd, step) : w3_zero16);
+  };
+  auto store = [&](int buf, const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
+    unsigned char* sb = smem + buf * G::STAGE;
+    *reinterpret_cast<uint4*>(sb + dst_a) = a;
+    *reinterpret_cast<uint4*>(sb + xb.dst) = b;
+    *reinterpret_cast<uint4*>(sb + xc_.dst) = c;
+    if (last_x) *reinterpret_cast<uint4*>(sb + xd.dst) = d;
+  };
+
+  // fragments (as wgrad3x3_kernel): pixel p = (i, wo) = (p / Q, p % Q); tap (r, s) reads
+  // window row r·RPS + i at O[wo] (s = 0), E[wo] (s = 1), O[wo + 1] (s = 2)
+  const int q = c16 >> 2, pp = c16 & 3;
+  const int p_lo = 8 * h4 + q, p_hi = p_lo + 4;
+  auto lane_off = [&](int row, int col0) {
+    const int col = col0 + 4 * pp;
+    return w3_off(row, col >> 3) + (col & 7) * 2;
+  };
+  auto xrow = [&](int px, int r, int s_) {
+    const int i = px / Q, wo = px % Q;
+    return (r * RPS + i) * G::PT + (s_ == 1 ? Q + 1 + wo : wo + (s_ >> 1));
+  };
+  int ao_lo[2], ao_hi[2], bo_lo[9], bo_hi[9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    ao_lo[i] = lane_off(p_lo, wm * 32 + 16 * i);
+    ao_hi[i] = lane_off(p_hi, wm * 32 + 16 * i);
+  }
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int n = wn * 144 + 16 * j;
+    const int t = n >> 6, r = t / 3, s_ = t - 3 * r;
+    bo_lo[j] = W3_DY_BYTES + lane_off(xrow(p_lo, r, s_), n & 63);
+    bo_hi[j] = W3_DY_BYTES + lane_off(xrow(p_hi, r, s_), n & 63);
+  }
+  auto frag = [&](const unsigned char* base, int o_lo, int o_hi) -> bf16x8 {
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_lo));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_hi));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
+    const unsigned char* base = smem + buf * G::STAGE;
+    bf16x8 af[2], bfr[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) bfr[j] = frag(base, bo_lo[j], bo_hi[j]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = frag(base, ao_lo[i], ao_hi[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
+
+  // K loop (wgrad3x3_kernel's, with a 2-step register ring): compute step k from buffer k&1,
+  // move step k+1 from its slot into the other buffer, refill the slot with step k+3
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto iter = [&](int base, auto U) {
+    constexpr int u = decltype(U)::value;
+    compute(u);
+    if constexpr (u == 0) {   // slot 1 holds step base+1
+      store(1, ra1, rb1, rc1, rd1);
+      load(base + 3, ra1, rb1, rc1, rd1);
+    } else {                  // slot 0 holds step base+2
+      store(0, ra0, rb0, rc0, rd0);
+      load(base + 4, ra0, rb0, rc0, rd0);
+    }
+    __syncthreads();
+  };
+  load(s_begin, ra0, rb0, rc0, rd0);
+  load(s_begin + 1, ra1, rb1, rc1, rd1);
+  store(0, ra0, rb0, rc0, rd0);
+  load(s_begin + 2, ra0, rb0, rc0, rd0);
+  __syncthreads();
+  for (int base = s_begin; base < s_end; base += 2) {
+    iter(base, I0{});
+    iter(base, I1{});
+  }
+
+  const int Ncol = 9 * p.C;
+  float* out = p.part + (size_t)split * p.K * Ncol;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = k0 + wm * 32 + 16 * i + c16;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int n = wn * 144 + 16 * j + 4 * h4;
+      const int t = n >> 6;
+      const f32x4 a = acc[i][j];
+      st16<SDX_NT_PART != 0>(out + (size_t)m * Ncol + t * p.C + c0 + (n & 63),
+                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                        __float_as_uint(a[3])));
+    }
+  }
+}
+
 bool w3_pipe_enabled(const ConvGeom& g) {
   static const bool on = [] {
     const char* e = getenv("SDX_W3_PIPE");
@@ -459,14 +645,20 @@ bool w3_pipe_enabled(const ConvGeom& g) {
 }  // namespace
 
 bool wgrad3x3_supported(const ConvGeom& g) {
-  const bool w_ok = g.W == 4 || g.W == 8 || g.W == 16 || g.W == 32;
-  return g.R == 3 && g.S == 3 && g.stride == 1 && g.pad == 1 && w_ok && g.H == g.W && g.P == g.H && g.Q == g.W &&
-         g.C % 64 == 0 && g.K % 64 == 0 && ((long)g.N * g.H * g.W) % 32 == 0;
+  static const bool s2_on = [] {   // SDX_W3_S2=0: stride-2 3x3 wgrads on the generic kernel
+    const char* e = getenv("SDX_W3_S2");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const bool q_ok = g.Q == 4 || g.Q == 8 || g.Q == 16 || g.Q == 32;
+  const bool geo = g.stride == 1 ? (g.P == g.H && g.Q == g.W)
+                                 : (s2_on && g.stride == 2 && g.H == 2 * g.P && g.W == 2 * g.Q);
+  return g.R == 3 && g.S == 3 && g.pad == 1 && q_ok && g.P == g.Q && geo && g.C % 64 == 0 && g.K % 64 == 0 &&
+         ((long)g.N * g.P * g.Q) % 32 == 0;
 }
 
 int wgrad3x3_tiles(const ConvGeom& g) { return (g.K / 64) * (g.C / 64); }
 
-int wgrad3x3_steps(const ConvGeom& g) { return (int)((long)g.N * g.H * g.W / 32); }
+int wgrad3x3_steps(const ConvGeom& g) { return (int)((long)g.N * g.P * g.Q / 32); }
 
 hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s) {
@@ -486,7 +678,14 @@ hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, flo
   if (!direct && partial == nullptr) return hipErrorInvalidValue;
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W3_NT);
-  if (w3_pipe_enabled(g)) {
+  if (g.stride == 2) {
+    switch (g.Q) {
+      case 4: hipLaunchKernelGGL(wgrad3x3_s2_kernel<4>, grid, block, 0, s, p); break;
+      case 8: hipLaunchKernelGGL(wgrad3x3_s2_kernel<8>, grid, block, 0, s, p); break;
+      case 16: hipLaunchKernelGGL(wgrad3x3_s2_kernel<16>, grid, block, 0, s, p); break;
+      default: hipLaunchKernelGGL(wgrad3x3_s2_kernel<32>, grid, block, 0, s, p); break;
+    }
+  } else if (w3_pipe_enabled(g)) {
     const dim3 pblock(W3P_NT);
     switch (g.W) {
       case 4: hipLaunchKernelGGL(wgrad3x3_pipe_kernel<4>, grid, pblock, 0, s, p); break;
