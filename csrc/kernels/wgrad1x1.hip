@@ -30,6 +30,13 @@ using namespace sdx;
 
 namespace {
 
+// SDX_W1_ORDER=1 (build define): issue a step's LDS traffic and refill loads before its
+// MFMAs in wgrad1x1_pipe_kernel. Measured 2-3 % slower per kernel than the compiler's order
+// (47.3 -> 48.5 us, profiles/wgrad_order_r4.txt), so off; the 3x3 kernels gain (SDX_W3_ORDER)
+#ifndef SDX_W1_ORDER
+#define SDX_W1_ORDER 0
+#endif
+
 constexpr int W1_NT = 512;      // 8 waves: 2 (output rows) x 4 (output columns)
 constexpr int W1_BM = 128;      // output channels (dW rows) per block
 constexpr int W1_PF = 4;        // steps of loads in flight (register ring of 4 named slots)
@@ -353,6 +360,20 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   auto iter = [&](int b0, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
     using S = std::integral_constant<int, (u + 2) % 4>;
+#if SDX_W1_ORDER
+    // every LDS access of the step (next fragments, the store of step k+2) and the refill
+    // loads are ISSUED before this step's MFMAs, so they complete under them: left to
+    // itself the scheduler put the fragment reads after the MFMAs, and the barrier's
+    // lgkmcnt(0) then exposed their whole latency plus the store transfer every step
+    if constexpr ((u & 1) == 0) read_frags(b_nxt, fa1, fb1);
+    else read_frags(b_nxt, fa0, fb0);
+    store(b_st, slot(S{}));
+    load(b0 + u + 6, slot(S{}));
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((u & 1) == 0) mfmas(fa0, fb0);
+    else mfmas(fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);   // (the MFMAs would otherwise sink past the barrier)
+#else
     if constexpr ((u & 1) == 0) {
       read_frags(b_nxt, fa1, fb1);
       mfmas(fa0, fb0);
@@ -362,6 +383,7 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
     }
     store(b_st, slot(S{}));
     load(b0 + u + 6, slot(S{}));
+#endif
     __syncthreads();
     unsigned char* t = b_cur;
     b_cur = b_nxt;

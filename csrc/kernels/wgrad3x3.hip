@@ -34,6 +34,14 @@ using namespace sdx;
 
 namespace {
 
+// SDX_W3_ORDER (default 1): a step's LDS stores and refill loads are issued before its
+// fragment reads and MFMAs (sched_barrier-pinned; otherwise the stores trail the MFMAs and
+// the barrier's lgkmcnt(0) waits for them): 6-8 % faster per kernel (81.7 vs 88.5 us at l3,
+// profiles/wgrad_order_r4.txt); 0 = the compiler's order
+#ifndef SDX_W3_ORDER
+#define SDX_W3_ORDER 1
+#endif
+
 constexpr int W3_NT = 512;      // 8 waves: 2 (output channels) x 4 (columns)
 constexpr int W3_ROWB = 128;    // LDS row: 64 bf16
 constexpr int W3_DY_BYTES = 32 * W3_ROWB;
@@ -42,6 +50,9 @@ constexpr int W3_PF = 4;        // steps of loads in flight (register ring of 4 
 typedef __attribute__((address_space(3))) bf16x4 w3_lds_bf16x4;
 
 __device__ __attribute__((aligned(16))) uint16_t w3_zero16[8];
+typedef const __attribute__((address_space(1))) uint16_t* w3_gptr;
+typedef unsigned int w3_u32x4 __attribute__((ext_vector_type(4)));   // (a HIP uint4 cannot be read
+typedef const __attribute__((address_space(1))) w3_u32x4* w3_g16;     //  through an AS-1 pointer)
 
 // byte offset of 16-B chunk ch of LDS row R
 __device__ __forceinline__ int w3_off(int R, int ch) {
@@ -100,20 +111,25 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   // base + step·stride plus, for x, the validity of its source row. Steps at or past s_end
   // (the unrolled loop's tail) load the zero page: they add nothing.
   // x-window chunk e (0..767): channel chunk e%8 of pixel w of window row ri = (r, i)
+  // zero page pinned in an SGPR pair: otherwise every select re-materialises its address
+  // (s_getpc + a GOT load + lgkmcnt(0), which also drains this wave's LDS traffic) and the
+  // divergent selects become exec-masked branches
+  w3_gptr zp = (w3_gptr)w3_zero16;
+  asm volatile("" : "+s"(zp));
   struct XChunk {
-    const uint16_t* base;   // x element of step 0 (may lie outside x: used only when valid)
-    int i, r;               // window image row within the step, tap row
+    w3_gptr base;   // x element of step 0 (may lie outside x: used only when valid)
+    int i, r;       // window image row within the step, tap row
   };
   auto x_chunk = [&](int e) -> XChunk {
     const int ch = e & 7, rest = e >> 3;
     const int w = rest % W, ri = rest / W;
     const int r = ri / RPS, i = ri % RPS;
-    return {p.x + ((long)(i + r - 1) * W + w) * p.C + c0 + ch * 8, i, r};
+    return {(w3_gptr)p.x + ((long)(i + r - 1) * W + w) * p.C + c0 + ch * 8, i, r};
   };
-  auto x_src = [&](const XChunk& xc, int step) -> const uint16_t* {
+  auto x_src = [&](const XChunk& xc, int step) -> w3_gptr {
     const int hs = ((step * RPS + xc.i) & (W - 1)) + xc.r - 1;   // H == W
     const bool ok = step < s_end && (unsigned)hs < (unsigned)W;
-    return ok ? xc.base + (long)step * 32 * p.C : w3_zero16;
+    return ok ? xc.base + (long)step * 32 * p.C : zp;
   };
   auto x_dst = [&](int e) -> int {
     const int ch = e & 7, rest = e >> 3;
@@ -124,30 +140,30 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   const int dst0 = first_dy ? w3_off(tid >> 3, tid & 7) : x_dst(e0);
   const int dst1 = x_dst(e1);
   const XChunk xc0 = x_chunk(first_dy ? 0 : e0), xc1 = x_chunk(e1);
-  const uint16_t* dy_base = p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
+  const w3_gptr dy_base = (w3_gptr)p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
   // register ring of 4 prefetched steps: slot u holds the step ≡ s_begin + u (mod 4). Named
   // registers selected at compile time (an array indexed inside the lambdas goes to scratch)
-  uint4 ra0, rb0, ra1, rb1, ra2, rb2, ra3, rb3;
-  auto slot_a = [&](auto U) -> uint4& {
+  w3_u32x4 ra0, rb0, ra1, rb1, ra2, rb2, ra3, rb3;
+  auto slot_a = [&](auto U) -> w3_u32x4& {
     if constexpr (decltype(U)::value == 0) return ra0;
     else if constexpr (decltype(U)::value == 1) return ra1;
     else if constexpr (decltype(U)::value == 2) return ra2;
     else return ra3;
   };
-  auto slot_b = [&](auto U) -> uint4& {
+  auto slot_b = [&](auto U) -> w3_u32x4& {
     if constexpr (decltype(U)::value == 0) return rb0;
     else if constexpr (decltype(U)::value == 1) return rb1;
     else if constexpr (decltype(U)::value == 2) return rb2;
     else return rb3;
   };
-  auto load = [&](int step, uint4& a, uint4& b) {
-    const uint16_t* s0 = first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : w3_zero16) : x_src(xc0, step);
-    a = *reinterpret_cast<const uint4*>(s0);
-    b = *reinterpret_cast<const uint4*>(x_src(xc1, step));
+  auto load = [&](int step, w3_u32x4& a, w3_u32x4& b) {
+    const w3_gptr s0 = first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : zp) : x_src(xc0, step);
+    a = *(w3_g16)s0;
+    b = *(w3_g16)x_src(xc1, step);
   };
-  auto store = [&](int buf, const uint4& a, const uint4& b) {
-    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + dst0) = a;
-    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + dst1) = b;
+  auto store = [&](int buf, const w3_u32x4& a, const w3_u32x4& b) {
+    *reinterpret_cast<w3_u32x4*>(smem + buf * G::STAGE + dst0) = a;
+    *reinterpret_cast<w3_u32x4*>(smem + buf * G::STAGE + dst1) = b;
   };
 
   // ---- fragment addressing: lane (h4, c16 = 4q + pp) reads K rows (pixels) 8h4+q and +4,
@@ -215,9 +231,19 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   auto iter = [&](int base, auto U) {
     constexpr int u = decltype(U)::value;
     using N = std::integral_constant<int, (u + 1) % W3_PF>;
+#if SDX_W3_ORDER
+    // the store of step k+1 (other buffer) and the refill loads issue before step k's
+    // fragment reads + MFMAs and complete under them instead of in front of the barrier
+    store((u + 1) & 1, slot_a(N{}), slot_b(N{}));
+    load(base + u + 1 + W3_PF, slot_a(N{}), slot_b(N{}));
+    __builtin_amdgcn_sched_barrier(0);
+    compute(u & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#else
     compute(u & 1);
     store((u + 1) & 1, slot_a(N{}), slot_b(N{}));
     load(base + u + 1 + W3_PF, slot_a(N{}), slot_b(N{}));
+#endif
     __syncthreads();
   };
   load(s_begin, ra0, rb0);
@@ -264,7 +290,6 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
 // buffer step k-1 vacated — one barrier per step, no fragment-read latency in front of the
 // MFMAs. Loads use 32-bit element offsets + a scalar step offset (host check: P·K, P·C <
 // 2^31) and select the zero page through an SGPR pair the compiler cannot rematerialise.
-typedef const __attribute__((address_space(1))) uint16_t* w3_gptr;
 constexpr int W3P_NT = 256;
 
 template <int W>
@@ -501,8 +526,10 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
   // chunk f%8), else x chunk e = f − 256: channel chunk e%8 of input column e/8 % 2Q of
   // window row ri = e/(16Q) = (r, i). Output row Rg = step·RPS + i (global over images, H =
   // 2P) reads input row 2Rg + r − 1: x element base + step·(2·RPS·W·C)
+  w3_gptr zp = (w3_gptr)w3_zero16;   // pinned in SGPRs (see wgrad3x3_kernel)
+  asm volatile("" : "+s"(zp));
   struct XChunk {
-    const uint16_t* base;   // element of step 0 (used only when valid)
+    w3_gptr base;   // element of step 0 (used only when valid)
     int i, r, dst;
   };
   auto x_chunk = [&](int e) -> XChunk {
@@ -510,35 +537,34 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
     const int col = rest % W, ri = rest / W;
     const int r = ri / RPS, i = ri % RPS;
     const int lrow = ri * G::PT + ((col & 1) ? (col + 1) >> 1 : Q + 1 + (col >> 1));
-    return {p.x + ((long)(2 * i + r - 1) * W + col) * p.C + c0 + ch * 8, i, r, W3_DY_BYTES + w3_off(lrow, ch)};
+    return {(w3_gptr)p.x + ((long)(2 * i + r - 1) * W + col) * p.C + c0 + ch * 8, i, r, W3_DY_BYTES + w3_off(lrow, ch)};
   };
   const long x_step = 2L * RPS * W * p.C;
-  auto x_src = [&](const XChunk& xc, int step) -> const uint16_t* {
+  auto x_src = [&](const XChunk& xc, int step) -> w3_gptr {
     const int hi = 2 * ((step * RPS + xc.i) & (Q - 1)) + xc.r - 1;   // input row within the image
     const bool ok = step < s_end && (unsigned)hi < (unsigned)W;
-    return ok ? xc.base + (long)step * x_step : w3_zero16;
+    return ok ? xc.base + (long)step * x_step : zp;
   };
   const bool first_dy = tid < 256, last_x = tid < 256;
   const XChunk xa = x_chunk(first_dy ? 0 : tid - 256), xb = x_chunk(tid + 256), xc_ = x_chunk(tid + 768),
                xd = x_chunk(last_x ? tid + 1280 : 0);
   const int dst_a = first_dy ? w3_off(tid >> 3, tid & 7) : xa.dst;
-  const uint16_t* dy_base = p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
-  // 2-step register ring of named uint4s (a struct of uint4 read through the lambdas ends up
+  const w3_gptr dy_base = (w3_gptr)p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
+  // 2-step register ring of named vectors (a struct of uint4 read through the lambdas ends up
   // in scratch)
-  uint4 ra0, rb0, rc0, rd0, ra1, rb1, rc1, rd1;
-  auto load = [&](int step, uint4& a, uint4& b, uint4& c, uint4& d) {
-    a = *reinterpret_cast<const uint4*>(first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : w3_zero16)
-                                                 : x_src(xa, step));
-    b = *reinterpret_cast<const uint4*>(x_src(xb, step));
-    c = *reinterpret_cast<const uint4*>(x_src(xc_, step));
-    d = *reinterpret_cast<const uint4*>(last_x ? x_src(xd, step) : w3_zero16);
+  w3_u32x4 ra0, rb0, rc0, rd0, ra1, rb1, rc1, rd1;
+  auto load = [&](int step, w3_u32x4& a, w3_u32x4& b, w3_u32x4& c, w3_u32x4& d) {
+    a = *(w3_g16)(first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : zp) : x_src(xa, step));
+    b = *(w3_g16)x_src(xb, step);
+    c = *(w3_g16)x_src(xc_, step);
+    d = *(w3_g16)(last_x ? x_src(xd, step) : zp);
   };
-  auto store = [&](int buf, const uint4& a, const uint4& b, const uint4& c, const uint4& d) {
+  auto store = [&](int buf, const w3_u32x4& a, const w3_u32x4& b, const w3_u32x4& c, const w3_u32x4& d) {
     unsigned char* sb = smem + buf * G::STAGE;
-    *reinterpret_cast<uint4*>(sb + dst_a) = a;
-    *reinterpret_cast<uint4*>(sb + xb.dst) = b;
-    *reinterpret_cast<uint4*>(sb + xc_.dst) = c;
-    if (last_x) *reinterpret_cast<uint4*>(sb + xd.dst) = d;
+    *reinterpret_cast<w3_u32x4*>(sb + dst_a) = a;
+    *reinterpret_cast<w3_u32x4*>(sb + xb.dst) = b;
+    *reinterpret_cast<w3_u32x4*>(sb + xc_.dst) = c;
+    if (last_x) *reinterpret_cast<w3_u32x4*>(sb + xd.dst) = d;
   };
 
   // fragments (as wgrad3x3_kernel): pixel p = (i, wo) = (p / Q, p % Q); tap (r, s) reads
@@ -596,7 +622,9 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
   using I1 = std::integral_constant<int, 1>;
   auto iter = [&](int base, auto U) {
     constexpr int u = decltype(U)::value;
+#if !SDX_W3_ORDER
     compute(u);
+#endif
     if constexpr (u == 0) {   // slot 1 holds step base+1
       store(1, ra1, rb1, rc1, rd1);
       load(base + 3, ra1, rb1, rc1, rd1);
@@ -604,6 +632,11 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
       store(0, ra0, rb0, rc0, rd0);
       load(base + 4, ra0, rb0, rc0, rd0);
     }
+#if SDX_W3_ORDER
+    __builtin_amdgcn_sched_barrier(0);
+    compute(u);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     __syncthreads();
   };
   load(s_begin, ra0, rb0, rc0, rd0);
