@@ -68,6 +68,7 @@ struct W3Params {
   int steps_total;      // N*H*W / 32
   int steps_per_split;
   int k_tiles, c_tiles, splits;
+  int h, w;             // image size (wgrad3x3_pad_kernel)
 };
 
 template <int W>
@@ -666,6 +667,173 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Stride-1 3x3 wgrad for image widths that are not a power of two (the 224x224 ImageNet-stem
+// ResNets: 56 / 28 / 14 / 7). The 32 pixel SLOTS of a step are RPS segments of SW = min(WS,
+// 32) slots, WS = the next power of two >= W: a segment is one image row (W <= 32, slots
+// w >= W hold zeros) or one half of a row (32 < W <= 64). Slot (i, c) of step k is column
+// w = half·SW + c of row Rg = G / SPR, G = k·RPS + i, half = G % SPR (SPR = WS / SW segments
+// per row); its dy row is read when w < W (else the zero page: it adds nothing). The x window
+// of segment i holds, for each tap row r, the SW + 2 columns half·SW − 1 … half·SW + SW of
+// image row Rg + r − 1, every one loaded with its own validity (image edge, w >= W), so a
+// half-row segment sees its real neighbours across the split. Fragment images, swizzle and
+// the schedule are wgrad3x3_s2_kernel's (2-step register ring, stores before the MFMAs).
+template <int WS>
+struct W3PadGeom {
+  static constexpr int SW = WS < 32 ? WS : 32;
+  static constexpr int SPR = WS / SW;                 // segments per image row
+  static constexpr int RPS = 32 / SW;                 // segments per step
+  static constexpr int P = SW == 32 ? 34 : SW == 16 ? 18 : 24;   // as W3Geom<SW>
+  static constexpr int XROWS = 3 * RPS * P;
+  static constexpr int STAGE = W3_DY_BYTES + XROWS * W3_ROWB;
+  static constexpr int XCH = 3 * RPS * (SW + 2) * 8;  // x chunks per step (816 / 864 / 960)
+  static_assert(XCH > 768 && XCH <= 1280, "loader layout: 3 chunks per thread");
+};
+
+template <int WS>
+__global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_pad_kernel(W3Params p) {
+  using G = W3PadGeom<WS>;
+  constexpr int SW = G::SW, SPR = G::SPR, RPS = G::RPS;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h4 = lane >> 4, c16 = lane & 15;
+  const int wm = wv >> 2, wn = wv & 3;
+  const int W = p.w, H = p.h;
+
+  const int tiles = p.k_tiles * p.c_tiles;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lin % tiles, split = lin / tiles;
+  const int k0 = (tile / p.c_tiles) * 64, c0 = (tile % p.c_tiles) * 64;
+  const int s_begin = split * p.steps_per_split;
+  const int s_end = min(p.steps_total, s_begin + p.steps_per_split);
+
+  w3_gptr zp = (w3_gptr)w3_zero16;   // pinned in SGPRs (see wgrad3x3_kernel)
+  asm volatile("" : "+s"(zp));
+  const w3_gptr gdy = (w3_gptr)p.dy, gx = (w3_gptr)p.x;
+  // loader: chunk f = tid + 512u (u < 3): f < 256 a dy chunk (slot f/8, channel chunk f%8),
+  // else x chunk e = f − 256 < XCH: channel chunk e%8 of window column e/8 % (SW+2) of window
+  // row e/(8(SW+2)) = (r, i)
+  struct Src {
+    int i, col, r, ch;   // segment in step, column within the segment (x: −1 … SW), tap row, chunk
+    bool x, has;
+    int dst;
+  };
+  auto chunk = [&](int f) -> Src {
+    if (f < 256) return {(f >> 3) / SW, (f >> 3) % SW, 1, f & 7, false, true, w3_off(f >> 3, f & 7)};
+    const int e = f - 256, ch = e & 7, rest = e >> 3;
+    const int cw = rest % (SW + 2), ri = rest / (SW + 2);
+    return {ri % RPS, cw - 1, ri / RPS, ch, true, e < G::XCH, W3_DY_BYTES + w3_off(ri * G::P + cw, ch)};
+  };
+  const Src sa = chunk(tid), sb = chunk(tid + 512), sc = chunk(tid + 1024);
+  auto src = [&](const Src& c, int step) -> w3_gptr {
+    const int seg = step * RPS + c.i;
+    const int rg = seg / SPR, w = (seg % SPR) * SW + c.col;   // image row (global), column
+    const int hs = rg % H + c.r - 1;                           // source row within the image
+    const bool ok = c.has && step < s_end && (unsigned)w < (unsigned)W && (unsigned)hs < (unsigned)H;
+    const long pix = (long)(rg + c.r - 1) * W + w;
+    return ok ? (c.x ? gx + pix * p.C + c0 + c.ch * 8 : gdy + pix * p.K + k0 + c.ch * 8) : zp;
+  };
+  w3_u32x4 ra0, rb0, rc0, ra1, rb1, rc1;
+  auto load = [&](int step, w3_u32x4& a, w3_u32x4& b, w3_u32x4& c) {
+    a = *(w3_g16)src(sa, step);
+    b = *(w3_g16)src(sb, step);
+    c = *(w3_g16)src(sc, step);
+  };
+  auto store = [&](int buf, const w3_u32x4& a, const w3_u32x4& b, const w3_u32x4& c) {
+    unsigned char* s_ = smem + buf * G::STAGE;
+    *reinterpret_cast<w3_u32x4*>(s_ + sa.dst) = a;
+    *reinterpret_cast<w3_u32x4*>(s_ + sb.dst) = b;
+    if (sc.has) *reinterpret_cast<w3_u32x4*>(s_ + sc.dst) = c;
+  };
+
+  // fragments: slot p = (i, c) = (p / SW, p % SW); tap (r, s) reads window row r·RPS + i,
+  // column c + s (window column 0 is the segment's column −1)
+  const int q = c16 >> 2, pp = c16 & 3;
+  const int p_lo = 8 * h4 + q, p_hi = p_lo + 4;
+  const int xb_lo = (p_lo / SW) * G::P + (p_lo % SW), xb_hi = (p_hi / SW) * G::P + (p_hi % SW);
+  auto lane_off = [&](int row, int col0) {
+    const int col = col0 + 4 * pp;
+    return w3_off(row, col >> 3) + (col & 7) * 2;
+  };
+  int ao_lo[2], ao_hi[2], bo_lo[9], bo_hi[9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    ao_lo[i] = lane_off(p_lo, wm * 32 + 16 * i);
+    ao_hi[i] = lane_off(p_hi, wm * 32 + 16 * i);
+  }
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int n = wn * 144 + 16 * j;
+    const int t = n >> 6, r = t / 3, s_ = t - 3 * r;
+    const int off = r * RPS * G::P + s_;
+    bo_lo[j] = W3_DY_BYTES + lane_off(xb_lo + off, n & 63);
+    bo_hi[j] = W3_DY_BYTES + lane_off(xb_hi + off, n & 63);
+  }
+  auto frag = [&](const unsigned char* base, int o_lo, int o_hi) -> bf16x8 {
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_lo));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_hi));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
+    const unsigned char* base = smem + buf * G::STAGE;
+    bf16x8 af[2], bfr[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) bfr[j] = frag(base, bo_lo[j], bo_hi[j]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = frag(base, ao_lo[i], ao_hi[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto iter = [&](int base, auto U) {
+    constexpr int u = decltype(U)::value;
+    if constexpr (u == 0) {   // slot 1 holds step base+1
+      store(1, ra1, rb1, rc1);
+      load(base + 3, ra1, rb1, rc1);
+    } else {                  // slot 0 holds step base+2
+      store(0, ra0, rb0, rc0);
+      load(base + 4, ra0, rb0, rc0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    compute(u);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  };
+  load(s_begin, ra0, rb0, rc0);
+  load(s_begin + 1, ra1, rb1, rc1);
+  store(0, ra0, rb0, rc0);
+  load(s_begin + 2, ra0, rb0, rc0);
+  __syncthreads();
+  for (int base = s_begin; base < s_end; base += 2) {
+    iter(base, I0{});
+    iter(base, I1{});
+  }
+
+  const int Ncol = 9 * p.C;
+  float* out = p.part + (size_t)split * p.K * Ncol;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = k0 + wm * 32 + 16 * i + c16;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int n = wn * 144 + 16 * j + 4 * h4;
+      const int t = n >> 6;
+      const f32x4 a = acc[i][j];
+      st16<SDX_NT_PART != 0>(out + (size_t)m * Ncol + t * p.C + c0 + (n & 63),
+                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                        __float_as_uint(a[3])));
+    }
+  }
+}
+
 bool w3_pipe_enabled(const ConvGeom& g) {
   static const bool on = [] {
     const char* e = getenv("SDX_W3_PIPE");
@@ -673,6 +841,19 @@ bool w3_pipe_enabled(const ConvGeom& g) {
   }();
   const long P = (long)g.N * g.H * g.W;   // 32-bit element offsets
   return on && P * g.K < (1L << 31) && P * g.C < (1L << 31);
+}
+
+// padded-slot kernel: slot width WS (next power of two >= W) for stride-1 widths that are not
+// one of {4, 8, 16, 32}
+int w3_pad_ws(const ConvGeom& g) {
+  static const bool on = [] {   // SDX_W3_PAD=0: those widths on the generic kernel
+    const char* e = getenv("SDX_W3_PAD");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (!on || g.stride != 1 || g.W == 4 || g.W == 8 || g.W == 16 || g.W == 32 || g.W < 5 || g.W > 64) return 0;
+  const int ws = g.W <= 8 ? 8 : g.W <= 16 ? 16 : g.W <= 32 ? 32 : 64;
+  const int sw = ws < 32 ? ws : 32, spr = ws / sw, rps = 32 / sw;
+  return ((long)g.N * g.H * spr) % rps == 0 ? ws : 0;
 }
 
 }  // namespace
@@ -685,13 +866,21 @@ bool wgrad3x3_supported(const ConvGeom& g) {
   const bool q_ok = g.Q == 4 || g.Q == 8 || g.Q == 16 || g.Q == 32;
   const bool geo = g.stride == 1 ? (g.P == g.H && g.Q == g.W)
                                  : (s2_on && g.stride == 2 && g.H == 2 * g.P && g.W == 2 * g.Q);
-  return g.R == 3 && g.S == 3 && g.pad == 1 && q_ok && g.P == g.Q && geo && g.C % 64 == 0 && g.K % 64 == 0 &&
-         ((long)g.N * g.P * g.Q) % 32 == 0;
+  const bool base = g.R == 3 && g.S == 3 && g.pad == 1 && g.P == g.Q && geo && g.C % 64 == 0 && g.K % 64 == 0;
+  if (base && g.stride == 1 && g.H == g.W && w3_pad_ws(g) > 0) return true;   // padded slots
+  return base && q_ok && ((long)g.N * g.P * g.Q) % 32 == 0;
 }
 
 int wgrad3x3_tiles(const ConvGeom& g) { return (g.K / 64) * (g.C / 64); }
 
-int wgrad3x3_steps(const ConvGeom& g) { return (int)((long)g.N * g.P * g.Q / 32); }
+int wgrad3x3_steps(const ConvGeom& g) {
+  const int ws = (g.stride == 1 && g.H == g.W) ? w3_pad_ws(g) : 0;
+  if (ws > 0) {   // segments of the padded-slot kernel / segments per step
+    const int sw = ws < 32 ? ws : 32;
+    return (int)((long)g.N * g.H * (ws / sw) / (32 / sw));
+  }
+  return (int)((long)g.N * g.P * g.Q / 32);
+}
 
 hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s) {
@@ -711,7 +900,17 @@ hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, flo
   if (!direct && partial == nullptr) return hipErrorInvalidValue;
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W3_NT);
-  if (g.stride == 2) {
+  p.h = g.H;
+  p.w = g.W;
+  const int ws = (g.stride == 1 && g.H == g.W) ? w3_pad_ws(g) : 0;
+  if (ws > 0) {
+    switch (ws) {
+      case 8: hipLaunchKernelGGL(wgrad3x3_pad_kernel<8>, grid, block, 0, s, p); break;
+      case 16: hipLaunchKernelGGL(wgrad3x3_pad_kernel<16>, grid, block, 0, s, p); break;
+      case 32: hipLaunchKernelGGL(wgrad3x3_pad_kernel<32>, grid, block, 0, s, p); break;
+      default: hipLaunchKernelGGL(wgrad3x3_pad_kernel<64>, grid, block, 0, s, p); break;
+    }
+  } else if (g.stride == 2) {
     switch (g.Q) {
       case 4: hipLaunchKernelGGL(wgrad3x3_s2_kernel<4>, grid, block, 0, s, p); break;
       case 8: hipLaunchKernelGGL(wgrad3x3_s2_kernel<8>, grid, block, 0, s, p); break;

@@ -135,6 +135,32 @@ def test_wgrad1x1_stream(gpu, shape, splits):
         assert torch.equal(m.conv_wgrad(dyh, xh, 1, 1, 1, 0, 0, -1), dw)
 
 
+@pytest.mark.parametrize("shape", [(4, 7, 64, 128), (3, 14, 128, 64), (2, 28, 64, 64), (2, 56, 64, 64),
+                                   (3, 12, 64, 64), (2, 40, 128, 64)])
+@pytest.mark.parametrize("splits", [1, 3, 0])
+def test_wgrad3x3_padded_width(gpu, shape, splits):
+    """Stride-1 tap-reuse 3x3 wgrad for widths that are not a power of two
+    (wgrad3x3_pad_kernel: 32 slots per step as rows padded to 8/16/32 slots, or half rows of
+    a 64-slot row — the 224x224 config's 56/28/14/7 and others) vs fp32 torch: direct,
+    split-K, auto split, accumulation into a sink, auto dispatch."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, C, K = shape
+    x, w = _mk(N, H, H, C, K, 3)
+    wf = w.float().requires_grad_(True)
+    out = F.conv2d(x.float(), wf, padding=1)
+    dy = torch.randn_like(out).bfloat16()
+    (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
+    dyh, xh = dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    dw = m.conv_wgrad(dyh, xh, 3, 3, 1, 1, splits, 9)
+    assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
+    sink = torch.full((K, 3, 3, C), 0.25, device=gpu)
+    m.conv_wgrad(dyh, xh, 3, 3, 1, 1, splits, 9, sink, True)
+    assert _rel(sink - 0.25, dw.float()) < 1e-5
+    if splits == 0:
+        assert torch.equal(m.conv_wgrad(dyh, xh, 3, 3, 1, 1, 0, -1), dw)
+
+
 @pytest.mark.parametrize("shape", [(4, 64, 64, 64), (4, 32, 128, 64), (3, 16, 64, 128), (4, 8, 128, 192)])
 @pytest.mark.parametrize("splits", [1, 3, 0])
 def test_wgrad3x3_stride2(gpu, shape, splits):
