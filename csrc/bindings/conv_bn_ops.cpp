@@ -449,7 +449,7 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     return e == nullptr || atoi(e) != 0;
   }();
   const bool w1 = (cfg == 10 || (cfg == -1 && w1_on && splits <= 0)) && !in_scale.has_value() && wgrad1x1_supported(g);
-  TORCH_CHECK(cfg != 10 || w1, "conv_wgrad: cfg 10 needs a 1x1 conv with K,C % 128 == 0 (stride 1, or stride s with H = s*P, W = s*Q, Q | 32)");
+  TORCH_CHECK(cfg != 10 || w1, "conv_wgrad: cfg 10 needs a 1x1 conv with K,C % 128 == 0 (stride 1, or stride s with H = s*P, W = s*Q)");
   // 64-output-channel GEMMs with a wide reduction side (layer-1 3x3: 64 x 576): the 64x256
   // tile (four 64x64 wave tiles) beats the exact-fit 64x64 one despite its padding, at
   // ~512 blocks (tools/wgrad_split_probe.py: 145 -> 124 us)

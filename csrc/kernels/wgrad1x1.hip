@@ -18,9 +18,9 @@
 // Shapes: K % 128 == 0, C % BN == 0 (BN = 256, or 128 when C is not a multiple of 256),
 // N·P·Q % 32 == 0 — layers 2-4 of the CIFAR/ImageNet ResNet bottlenecks (reference
 // networks/resnet_big.py:44-49, conv1/conv3 of each Bottleneck), and the strided projection
-// shortcuts (:50-55) when a step is whole output rows (pipelined kernel: each x chunk reads
-// its pixel at base + step·const). The layer-1 1x1 wgrads (64 channels on one side) are
-// HBM-bound and stay on the generic kernel.
+// shortcuts (:50-55) on the pipelined kernel (an x chunk reads its pixel at base + step·const
+// when a step is whole output rows, else from g / Q per step). The layer-1 1x1 wgrads (64
+// channels on one side) are HBM-bound and stay on the generic kernel.
 #include <type_traits>
 
 #include "common.h"
@@ -65,9 +65,14 @@ struct W1Params {
   int K, C;
   int steps_total;      // dy pixels / 32
   // x pixel of dy pixel j of a step (pipelined kernel): stride 1: j; stride st (H = st·P,
-  // W = st·Q, Q | 32): st·(W·(j / Q) + j % Q). x step stride in elements (32·C at stride 1)
+  // W = st·Q, Q | 32): st·(W·(j / Q) + j % Q). x step stride in elements (32·C at stride 1;
+  // 0 for the GEN kernels)
   int xst, xq, xw;
   int x_step;
+  // GEN kernels (a step is not whole output rows, 32 % Q != 0): the x pixel of step pixel
+  // g = 32·step + j is xst·(xw·(g / Q) + g % Q), with g / Q = umulhi(g, xmagic) (exact for
+  // g·Q < 2^32, host check)
+  unsigned xmagic;
   int steps_per_split;
   int k_tiles, c_tiles, splits;
 };
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_kernel(W1Params p) {
 // step k-1 vacated — one barrier per step, no LDS latency in front of the MFMAs. (An
 // LDS-DMA version of this kernel, 3-stage ring of 64-pixel steps, measured 12-48 % slower
 // per kernel: profiles/ablate_wgrad_r3.txt.)
-template <int BN>
+template <int BN, bool GEN>
 __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   constexpr int A_BYTES = 32 * W1_BM * 2;
   constexpr int STAGE = A_BYTES + 32 * BN * 2;
@@ -273,6 +278,12 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   auto xpix = [&](int j) { return p.xst * (p.xw * (j / p.xq) + j % p.xq); };
   const int x_off1 = xpix(e1 / B_CPR) * p.C + c0 + (e1 % B_CPR) * 8;
   const int x_off2 = xpix(e2 / B_CPR) * p.C + c0 + (e2 % B_CPR) * 8;
+  // GEN: element offset of x chunk e at step `step` (pixel g = 32·step + e / B_CPR)
+  auto xgen = [&](int step, int e) __attribute__((always_inline)) {
+    const unsigned g = 32u * (unsigned)step + (unsigned)(e / B_CPR);
+    const unsigned q = __umulhi(g, p.xmagic);
+    return (int)(p.xst * (p.xw * q + (g - q * p.xq))) * p.C + c0 + (e % B_CPR) * 8;
+  };
   const int x_dst1 = A_BYTES + w1_off<BN>(e1 / B_CPR, e1 % B_CPR);
   const int x_dst2 = A_BYTES + w1_off<BN>(e2 / B_CPR, e2 % B_CPR);
   const int sA = 32 * p.K, sB = p.x_step;
@@ -296,8 +307,13 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   auto load = [&](int step, Regs& r) __attribute__((always_inline)) {
     const bool ok = step < s_end;
     r.a = *(g16)(ok ? gdy + (a_off + step * sA) : zp);
-    r.b = *(g16)(ok ? gx + (x_off1 + step * sB) : zp);
-    if constexpr (NCH == 3) r.c = *(g16)(ok ? gx + (x_off2 + step * sB) : zp);
+    if constexpr (GEN) {
+      r.b = *(g16)(ok ? gx + xgen(step, e1) : zp);
+      if constexpr (NCH == 3) r.c = *(g16)(ok ? gx + xgen(step, e2) : zp);
+    } else {
+      r.b = *(g16)(ok ? gx + (x_off1 + step * sB) : zp);
+      if constexpr (NCH == 3) r.c = *(g16)(ok ? gx + (x_off2 + step * sB) : zp);
+    }
   };
   auto store = [&](unsigned char* sb, const Regs& r) __attribute__((always_inline)) {
     *reinterpret_cast<u32x4*>(sb + a_dst) = r.a;
@@ -446,14 +462,15 @@ bool w1_pipe_enabled(const ConvGeom& g) {
 
 // stride 1 (any image size), or a strided 1x1 (projection shortcut, reference
 // networks/resnet_big.py:50-55) on the pipelined kernel when the input is exactly st x the
-// output and a 32-pixel step is whole output rows (Q | 32: the x source of a step pixel is
-// then base + step·const)
+// output (Q | 32: the x source of a step pixel is base + step·const; otherwise the GEN
+// instantiation divides the step pixel index by Q)
 bool wgrad1x1_supported(const ConvGeom& g) {
   static const bool strided_on = [] {   // SDX_W1_STRIDED=0: strided shortcuts on the generic kernel
     const char* e = getenv("SDX_W1_STRIDED");
     return e == nullptr || atoi(e) != 0;
   }();
-  const bool strided_ok = strided_on && g.stride > 1 && g.H == g.stride * g.P && g.W == g.stride * g.Q && 32 % g.Q == 0 &&
+  const bool strided_ok = strided_on && g.stride > 1 && g.H == g.stride * g.P && g.W == g.stride * g.Q &&
+                          (long)g.N * g.P * g.Q * g.Q < (1L << 32) &&
                           w1_pipe_enabled(g);
   return g.R == 1 && g.S == 1 && g.pad == 0 && (g.stride == 1 ? (g.P == g.H && g.Q == g.W) : strided_ok) &&
          g.K % W1_BM == 0 && g.C % 128 == 0 && ((long)g.N * g.P * g.Q) % 32 == 0;
@@ -477,7 +494,8 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
     p.x_step = 32 * g.C;
   } else {
     p.xst = g.stride, p.xq = g.Q, p.xw = g.W;
-    p.x_step = g.stride * g.W * (32 / g.Q) * g.C;
+    p.x_step = 32 % g.Q == 0 ? g.stride * g.W * (32 / g.Q) * g.C : 0;
+    p.xmagic = (unsigned)((1ULL << 32) / (unsigned)g.Q + 1);
   }
   p.steps_per_split = (p.steps_total + splits - 1) / splits;
   p.splits = (p.steps_total + p.steps_per_split - 1) / p.steps_per_split;
@@ -489,8 +507,15 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W1_NT);
   if (w1_pipe_enabled(g)) {   // (a strided shape is supported only when it is)
-    if (bn == 256) hipLaunchKernelGGL(wgrad1x1_pipe_kernel<256>, grid, block, 0, s, p);
-    else hipLaunchKernelGGL(wgrad1x1_pipe_kernel<128>, grid, block, 0, s, p);
+    const bool gen = g.stride > 1 && 32 % g.Q != 0;
+    if (gen) {
+      if (bn == 256) hipLaunchKernelGGL((wgrad1x1_pipe_kernel<256, true>), grid, block, 0, s, p);
+      else hipLaunchKernelGGL((wgrad1x1_pipe_kernel<128, true>), grid, block, 0, s, p);
+    } else if (bn == 256) {
+      hipLaunchKernelGGL((wgrad1x1_pipe_kernel<256, false>), grid, block, 0, s, p);
+    } else {
+      hipLaunchKernelGGL((wgrad1x1_pipe_kernel<128, false>), grid, block, 0, s, p);
+    }
   } else if (bn == 256) {
     hipLaunchKernelGGL(wgrad1x1_kernel<256>, grid, block, 0, s, p);
   } else {

@@ -186,12 +186,14 @@ def test_wgrad3x3_stride2(gpu, shape, splits):
         assert torch.equal(m.conv_wgrad(dyh, xh, 3, 3, 2, 1, 0, -1), dw)
 
 
-@pytest.mark.parametrize("shape", [(4, 32, 256, 512), (8, 16, 512, 256), (16, 8, 256, 128), (4, 8, 128, 256)])
+@pytest.mark.parametrize("shape", [(4, 32, 256, 512), (8, 16, 512, 256), (16, 8, 256, 128), (4, 8, 128, 256),
+                                   (32, 14, 128, 256), (8, 28, 128, 128), (4, 56, 256, 128), (2, 24, 128, 128)])
 @pytest.mark.parametrize("splits", [1, 3, 0])
 def test_wgrad1x1_strided(gpu, shape, splits):
     """Stride-2 1x1 wgrad (projection shortcut, reference networks/resnet_big.py:50-55) on the
     pipelined 1x1 kernel (cfg 10): output widths 16 / 8 / 4 (a 32-pixel step is 2 / 4 / 8
-    output rows, crossing images at 4 and 8), vs fp32 torch; direct, split-K, auto, sink."""
+    output rows, crossing images at 4 and 8) and 7 / 14 / 28 / 12 (steps that are not whole
+    rows: the GEN instantiation's per-step g / Q), vs fp32 torch; direct, split-K, auto, sink."""
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
     N, H, C, K = shape
