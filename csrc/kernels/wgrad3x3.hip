@@ -500,10 +500,13 @@ struct W3S2Geom {
   static_assert(XCH == 1536, "loader layout");
 };
 
-template <int Q>
+// PAD: output width pq = p.w / 2 < Q slots (not a power of two: the 224x224 config's 28 / 14 /
+// 7 on 32 / 16 / 8 slots); slots c >= pq and input columns >= 2·pq read the zero page
+template <int Q, bool PAD>
 __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
   using G = W3S2Geom<Q>;
   constexpr int RPS = G::RPS, W = 2 * Q;
+  const int Wr = PAD ? p.w : W, pq = PAD ? p.w / 2 : Q;   // real input / output widths
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int h4 = lane >> 4, c16 = lane & 15;
@@ -532,30 +535,38 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_s2_kernel(W3Params p) {
   struct XChunk {
     w3_gptr base;   // element of step 0 (used only when valid)
     int i, r, dst;
+    bool cok;       // input column inside the image (PAD)
   };
   auto x_chunk = [&](int e) -> XChunk {
     const int ch = e & 7, rest = e >> 3;
     const int col = rest % W, ri = rest / W;
     const int r = ri / RPS, i = ri % RPS;
     const int lrow = ri * G::PT + ((col & 1) ? (col + 1) >> 1 : Q + 1 + (col >> 1));
-    return {(w3_gptr)p.x + ((long)(2 * i + r - 1) * W + col) * p.C + c0 + ch * 8, i, r, W3_DY_BYTES + w3_off(lrow, ch)};
+    return {(w3_gptr)p.x + ((long)(2 * i + r - 1) * Wr + col) * p.C + c0 + ch * 8, i, r, W3_DY_BYTES + w3_off(lrow, ch),
+            col < Wr};
   };
-  const long x_step = 2L * RPS * W * p.C;
+  const long x_step = 2L * RPS * Wr * p.C;
   auto x_src = [&](const XChunk& xc, int step) -> w3_gptr {
-    const int hi = 2 * ((step * RPS + xc.i) & (Q - 1)) + xc.r - 1;   // input row within the image
-    const bool ok = step < s_end && (unsigned)hi < (unsigned)W;
+    const int ho = PAD ? (step * RPS + xc.i) % pq : (step * RPS + xc.i) & (Q - 1);
+    const int hi = 2 * ho + xc.r - 1;   // input row within the image
+    const bool ok = step < s_end && (unsigned)hi < (unsigned)Wr && (!PAD || xc.cok);
     return ok ? xc.base + (long)step * x_step : zp;
   };
   const bool first_dy = tid < 256, last_x = tid < 256;
   const XChunk xa = x_chunk(first_dy ? 0 : tid - 256), xb = x_chunk(tid + 256), xc_ = x_chunk(tid + 768),
                xd = x_chunk(last_x ? tid + 1280 : 0);
   const int dst_a = first_dy ? w3_off(tid >> 3, tid & 7) : xa.dst;
-  const w3_gptr dy_base = (w3_gptr)p.dy + (long)(tid >> 3) * p.K + k0 + (tid & 7) * 8;
+  // dy slot j = tid/8 = (i, c) = (j / Q, j % Q): output pixel i·pq + c of the step (c < pq)
+  const int dslot = tid >> 3;
+  const bool dy_ok = !PAD || dslot % Q < pq;
+  const long dy_step = PAD ? (long)RPS * pq * p.K : 32L * p.K;
+  const w3_gptr dy_base =
+      (w3_gptr)p.dy + (long)(PAD ? (dslot / Q) * pq + dslot % Q : dslot) * p.K + k0 + (tid & 7) * 8;
   // 2-step register ring of named vectors (a struct of uint4 read through the lambdas ends up
   // in scratch)
   w3_u32x4 ra0, rb0, rc0, rd0, ra1, rb1, rc1, rd1;
   auto load = [&](int step, w3_u32x4& a, w3_u32x4& b, w3_u32x4& c, w3_u32x4& d) {
-    a = *(w3_g16)(first_dy ? (step < s_end ? dy_base + (long)step * 32 * p.K : zp) : x_src(xa, step));
+    a = *(w3_g16)(first_dy ? (step < s_end && dy_ok ? dy_base + (long)step * dy_step : zp) : x_src(xa, step));
     b = *(w3_g16)x_src(xb, step);
     c = *(w3_g16)x_src(xc_, step);
     d = *(w3_g16)(last_x ? x_src(xd, step) : zp);
@@ -856,6 +867,16 @@ int w3_pad_ws(const ConvGeom& g) {
   return ((long)g.N * g.H * spr) % rps == 0 ? ws : 0;
 }
 
+// stride-2 slots per output row: Q itself (4/8/16/32), else the next of 8/16/32 above it
+// (0: unsupported); a step is 32/slots whole output rows
+int w3_s2_slots(const ConvGeom& g) {
+  if (g.Q == 4 || g.Q == 8 || g.Q == 16 || g.Q == 32) return g.Q;
+  // (w3_pad_ws of the output-sized stride-1 geometry: honours SDX_W3_PAD)
+  if (g.Q < 5 || g.Q > 32 || !w3_pad_ws(ConvGeom{g.N, g.P, g.Q, g.C, g.K, 3, 3, g.P, g.Q, 1, 1})) return 0;
+  const int sq = g.Q <= 8 ? 8 : g.Q <= 16 ? 16 : 32;
+  return ((long)g.N * g.P) % (32 / sq) == 0 ? sq : 0;
+}
+
 }  // namespace
 
 bool wgrad3x3_supported(const ConvGeom& g) {
@@ -864,6 +885,9 @@ bool wgrad3x3_supported(const ConvGeom& g) {
     return e == nullptr || atoi(e) != 0;
   }();
   const bool q_ok = g.Q == 4 || g.Q == 8 || g.Q == 16 || g.Q == 32;
+  if (g.stride == 2 && s2_on && g.R == 3 && g.S == 3 && g.pad == 1 && g.P == g.Q && g.H == 2 * g.P &&
+      g.W == 2 * g.Q && g.C % 64 == 0 && g.K % 64 == 0 && !q_ok && w3_s2_slots(g) > 0)
+    return true;   // padded output rows
   const bool geo = g.stride == 1 ? (g.P == g.H && g.Q == g.W)
                                  : (s2_on && g.stride == 2 && g.H == 2 * g.P && g.W == 2 * g.Q);
   const bool base = g.R == 3 && g.S == 3 && g.pad == 1 && g.P == g.Q && geo && g.C % 64 == 0 && g.K % 64 == 0;
@@ -878,6 +902,10 @@ int wgrad3x3_steps(const ConvGeom& g) {
   if (ws > 0) {   // segments of the padded-slot kernel / segments per step
     const int sw = ws < 32 ? ws : 32;
     return (int)((long)g.N * g.H * (ws / sw) / (32 / sw));
+  }
+  if (g.stride == 2 && !(g.Q == 4 || g.Q == 8 || g.Q == 16 || g.Q == 32)) {   // padded rows
+    const int sq = w3_s2_slots(g);
+    return (int)((long)g.N * g.P / (32 / sq));
   }
   return (int)((long)g.N * g.P * g.Q / 32);
 }
@@ -911,11 +939,21 @@ hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, flo
       default: hipLaunchKernelGGL(wgrad3x3_pad_kernel<64>, grid, block, 0, s, p); break;
     }
   } else if (g.stride == 2) {
-    switch (g.Q) {
-      case 4: hipLaunchKernelGGL(wgrad3x3_s2_kernel<4>, grid, block, 0, s, p); break;
-      case 8: hipLaunchKernelGGL(wgrad3x3_s2_kernel<8>, grid, block, 0, s, p); break;
-      case 16: hipLaunchKernelGGL(wgrad3x3_s2_kernel<16>, grid, block, 0, s, p); break;
-      default: hipLaunchKernelGGL(wgrad3x3_s2_kernel<32>, grid, block, 0, s, p); break;
+    const bool pad = !(g.Q == 4 || g.Q == 8 || g.Q == 16 || g.Q == 32);
+    const int sq = w3_s2_slots(g);
+    if (pad) {
+      switch (sq) {
+        case 8: hipLaunchKernelGGL((wgrad3x3_s2_kernel<8, true>), grid, block, 0, s, p); break;
+        case 16: hipLaunchKernelGGL((wgrad3x3_s2_kernel<16, true>), grid, block, 0, s, p); break;
+        default: hipLaunchKernelGGL((wgrad3x3_s2_kernel<32, true>), grid, block, 0, s, p); break;
+      }
+    } else {
+      switch (g.Q) {
+        case 4: hipLaunchKernelGGL((wgrad3x3_s2_kernel<4, false>), grid, block, 0, s, p); break;
+        case 8: hipLaunchKernelGGL((wgrad3x3_s2_kernel<8, false>), grid, block, 0, s, p); break;
+        case 16: hipLaunchKernelGGL((wgrad3x3_s2_kernel<16, false>), grid, block, 0, s, p); break;
+        default: hipLaunchKernelGGL((wgrad3x3_s2_kernel<32, false>), grid, block, 0, s, p); break;
+      }
     }
   } else if (w3_pipe_enabled(g)) {
     const dim3 pblock(W3P_NT);

@@ -161,12 +161,14 @@ def test_wgrad3x3_padded_width(gpu, shape, splits):
         assert torch.equal(m.conv_wgrad(dyh, xh, 3, 3, 1, 1, 0, -1), dw)
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 64, 64), (4, 32, 128, 64), (3, 16, 64, 128), (4, 8, 128, 192)])
+@pytest.mark.parametrize("shape", [(4, 64, 64, 64), (4, 32, 128, 64), (3, 16, 64, 128), (4, 8, 128, 192),
+                                   (4, 14, 64, 128), (3, 28, 128, 64), (2, 56, 64, 64), (3, 24, 64, 64)])
 @pytest.mark.parametrize("splits", [1, 3, 0])
 def test_wgrad3x3_stride2(gpu, shape, splits):
     """Stride-2 tap-reuse 3x3 wgrad (wgrad3x3_s2_kernel: de-interleaved x window; the first
     3x3 of layers 2-4, reference networks/resnet_big.py:45) vs fp32 torch: output widths
-    32 / 16 / 8 / 4 (a 32-pixel step is 1 / 2 / 4 / 8 output rows, crossing images at 8 and 4),
+    32 / 16 / 8 / 4 (a 32-pixel step is 1 / 2 / 4 / 8 output rows, crossing images at 8 and 4)
+    and 7 / 14 / 28 / 12 on padded rows of 8 / 16 / 32 / 16 slots (the 224x224 config),
     direct / split-K / auto split, accumulation into a sink, auto dispatch."""
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
