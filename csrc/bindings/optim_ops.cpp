@@ -42,9 +42,18 @@ void lars_step(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tenso
             "lars_step");
 }
 
+// zero a contiguous GPU buffer with the runtime's fill (hipMemsetAsync on the current stream):
+// the flat gradient buffer's per-step reset without a torch elementwise kernel in the step
+void zero_async(torch::Tensor t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_async: contiguous GPU tensor");
+  c10::DeviceGuard dg(t.device());
+  check_hip(hipMemsetAsync(t.data_ptr(), 0, t.nbytes(), cur_stream()), "zero_async");
+}
+
 }  // namespace
 
 void register_optim(pybind11::module& m) {
+  m.def("zero_async", &zero_async, "hipMemsetAsync(0) of a contiguous GPU tensor on the current stream");
   m.def("sgd_step", &sgd_step, "fused flat-buffer SGD (momentum, wd, grad scale, device lr)", pybind11::arg("p"),
         pybind11::arg("g"), pybind11::arg("buf"), pybind11::arg("lr"), pybind11::arg("momentum"), pybind11::arg("wd"),
         pybind11::arg("gscale"), pybind11::arg("nesterov"), pybind11::arg("max_blocks") = 0);

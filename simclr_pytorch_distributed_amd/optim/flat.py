@@ -72,7 +72,11 @@ class FlatParams:
                 p.grad = g
 
     def zero_grad(self):
-        self.grad.zero_()
+        # one runtime fill on the step stream (hipMemsetAsync), not a torch FillFunctor kernel
+        if self.grad.is_cuda and _ext.available():
+            _ext.require().zero_async(self.grad)
+        else:
+            self.grad.zero_()
 
     def segment_table(self):
         offs = [self.offsets[i] for i in self.order]
