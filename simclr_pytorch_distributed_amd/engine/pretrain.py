@@ -307,7 +307,8 @@ class PretrainEngine:
             if prefetch is not None:
                 prefetch()          # weight conversion overlaps the augmentation launch
             x = self.make_views(idx, epoch, it)
-            labels = self.labels[idx]
+            # (SimCLR ignores labels: no gather kernel in its step)
+            labels = self.labels[idx] if opt.method == "SupCon" else None
         with ph("forward"):
             feats = self.runner.forward(x)
         with ph("loss"):
