@@ -74,6 +74,30 @@ std::vector<torch::Tensor> supcon_bwd(torch::Tensor A, torch::Tensor C, torch::T
   return {dA, dC};
 }
 
+// anchors == contrasts (single rank, contrast_mode all): the gradient w.r.t. the one
+// feature tensor, dA + dC summed in the split reduction (one launch less, no add kernel)
+torch::Tensor supcon_bwd_sum(torch::Tensor X, torch::Tensor a_self, torch::Tensor a_key, torch::Tensor c_key,
+                             torch::Tensor lse, torch::Tensor invcnt, torch::Tensor g, double inv_temp, double w) {
+  check_rows(X, "X");
+  const int64_t N = X.size(0), D = X.size(1);
+  TORCH_CHECK(D == 64 || D == 128 || D == 256, "bad feature dim");
+  check_idx(a_self, N, "a_self");
+  check_idx(a_key, N, "a_key");
+  check_idx(c_key, N, "c_key");
+  TORCH_CHECK(lse.is_cuda() && lse.numel() == N && invcnt.numel() == N, "lse/invcnt shape");
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.numel() == 1, "g must be a GPU float scalar");
+  c10::DeviceGuard dg(X.device());
+  auto gc = g.contiguous();
+  auto dX = torch::empty_like(X);
+  auto ws = torch::empty({std::max<long>(1, supcon_bwd_sum_workspace((int)N, (int)D))}, X.options());
+  check_hip(launch_supcon_bwd_sum(X.data_ptr<float>(), a_self.data_ptr<int>(), a_key.data_ptr<int>(),
+                                  c_key.data_ptr<int>(), lse.data_ptr<float>(), invcnt.data_ptr<float>(), (int)N,
+                                  (int)D, (float)inv_temp, (float)w, gc.data_ptr<float>(), dX.data_ptr<float>(),
+                                  ws.data_ptr<float>(), cur_stream()),
+            "supcon_bwd_sum");
+  return dX;
+}
+
 // F.normalize(x, dim=1) as one launch: returns (y, row norms)
 std::vector<torch::Tensor> rownorm_fwd(torch::Tensor x, double eps) {
   check_rows(x, "x");
@@ -129,6 +153,7 @@ void register_supcon(pybind11::module& m) {
   m.def("norm_stats", &norm_stats, "SEC/L2-reg feature-norm statistics + record_norm_mean EMA (one launch)");
   m.def("supcon_fwd", &supcon_fwd, "fused SupCon/NT-Xent forward (row form)");
   m.def("supcon_bwd", &supcon_bwd, "fused SupCon/NT-Xent backward (row form)");
+  m.def("supcon_bwd_sum", &supcon_bwd_sum, "SupCon backward when anchors are the contrasts: dA + dC in one reduce");
 }
 
 }  // namespace sdx_bind

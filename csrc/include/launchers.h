@@ -24,6 +24,12 @@ hipError_t launch_supcon_fwd(const float* A, const float* C, const int* a_self, 
                              float* row_loss, float* loss, hipStream_t s);
 // ws: fp32 workspace of supcon_bwd_workspace(Na, N, D) elements (per-split partial slabs)
 long supcon_bwd_workspace(int Na, int N, int D);
+// anchors == contrasts (one [N][D] tensor): dX = dA + dC through one split reduction;
+// ws: supcon_bwd_sum_workspace(N, D) elements
+long supcon_bwd_sum_workspace(int N, int D);
+hipError_t launch_supcon_bwd_sum(const float* X, const int* a_self, const int* a_key, const int* c_key,
+                                 const float* lse, const float* invcnt, int N, int D, float inv_temp, float w,
+                                 const float* gscale, float* dX, float* ws, hipStream_t s);
 hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, const int* a_key,
                              const int* c_key, const float* lse, const float* invcnt, int Na, int N, int D,
                              float inv_temp, float w, const float* gscale, float* dA, float* dC, float* ws,

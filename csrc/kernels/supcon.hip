@@ -446,6 +446,34 @@ hipError_t launch_supcon_fwd(const float* A, const float* C, const int* a_self, 
   return hipSuccess;
 }
 
+// anchors == contrasts (single rank, contrast_mode all: A and C are one tensor): d(A) + d(C)
+// in ONE reduction — both passes write split slabs of the same [N][D] layout back to back,
+// and one split reduce sums all of them (no separate reduce per pass, no elementwise add)
+long supcon_bwd_sum_workspace(int N, int D) {
+  int per;
+  return (long)2 * bwd_splits(N, N, &per) * N * D;
+}
+
+hipError_t launch_supcon_bwd_sum(const float* X, const int* a_self, const int* a_key, const int* c_key,
+                                 const float* lse, const float* invcnt, int N, int D, float inv_temp, float w,
+                                 const float* gscale, float* dX, float* ws, hipStream_t s) {
+  SupconParams p{};
+  p.gscale = gscale;
+  p.a_self = a_self; p.a_key = a_key; p.c_key = c_key; p.lse = lse; p.invcnt = invcnt;
+  p.inv_temp = inv_temp; p.w = w;
+  p.own = X; p.other = X; p.n_own = N; p.n_other = N;
+  const int sa = bwd_splits(N, N, &p.other_per_split);
+  p.n_split = sa;
+  p.out = ws;
+  hipError_t e = launch_mode<MODE_BWD_A>(D, p, s);
+  if (e != hipSuccess) return e;
+  const int sc = bwd_splits(N, N, &p.other_per_split);
+  p.n_split = sc;
+  p.out = ws + (long)sa * N * D;
+  if ((e = launch_mode<MODE_BWD_C>(D, p, s)) != hipSuccess) return e;
+  return split_reduce(ws, sa + sc, (long)N * D, dX, s);
+}
+
 hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, const int* a_key,
                              const int* c_key, const float* lse, const float* invcnt, int Na, int N, int D,
                              float inv_temp, float w, const float* gscale, float* dA, float* dC, float* ws,

@@ -34,6 +34,9 @@ class _SupConRows(torch.autograd.Function):
         ctx.w = scale * ratio / temperature
         ctx.inv_temp = 1.0 / temperature
         ctx.dtypes = (A.dtype, C.dtype)
+        # one rank, contrast_mode "all": the anchors ARE the contrasts (one tensor) -> the
+        # backward sums dA + dC inside its split reduction
+        ctx.same = A is C and A32.shape[0] == C32.shape[0]
         ctx.mark_non_differentiable(row_loss)
         return loss.view(()), row_loss
 
@@ -42,6 +45,9 @@ class _SupConRows(torch.autograd.Function):
         m = _ext.require()
         A32, C32, si, ak, ck, lse, invcnt = ctx.saved_tensors
         gl = g.float().reshape(1).contiguous()
+        if ctx.same:
+            dX = m.supcon_bwd_sum(A32, si, ak, ck, lse, invcnt, gl, ctx.inv_temp, ctx.w)
+            return dX.to(ctx.dtypes[0]), None, None, None, None, None, None, None
         dA, dC = m.supcon_bwd(A32, C32, si, ak, ck, lse, invcnt, gl, ctx.inv_temp, ctx.w)
         return dA.to(ctx.dtypes[0]), dC.to(ctx.dtypes[1]), None, None, None, None, None, None
 

@@ -87,3 +87,24 @@ def test_supcon_backward_deterministic(gpu, na, n):
     got[:na] += outs[0][0].double()
     err = (got - Cr.grad).abs().max().item()
     assert err < 1e-4 * Cr.grad.abs().max().item() + 1e-7, err
+
+
+@pytest.mark.parametrize("n,D,supcon", [(256, 128, False), (100, 128, True), (2048, 128, False)])
+def test_supcon_backward_sum_when_anchors_are_contrasts(gpu, n, D, supcon):
+    """One rank, contrast_mode "all": the anchors ARE the contrast tensor, and the backward
+    sums dA + dC inside its split reduction (supcon_bwd_sum) instead of a separate reduce +
+    an autograd add. Same gradient as the two-output path (fp32 summation order aside) and
+    as the fp64 oracle."""
+    from simclr_pytorch_distributed_amd.ops.contrastive import supcon_rows_loss
+    C, self_idx, key = _case(n, D, supcon=supcon, mode="all")
+    temp, base = 0.5, 0.07
+    scale = 1.0 / self_idx.numel()
+    X = C.clone().requires_grad_(True)
+    supcon_rows_loss(X, X, self_idx, key, key, temp, base, scale).backward()      # merged
+    Y = C.clone().requires_grad_(True)
+    supcon_rows_loss(Y * 1.0, Y, self_idx, key, key, temp, base, scale).backward()  # two outputs
+    assert torch.allclose(X.grad, Y.grad, rtol=1e-5, atol=1e-7), (X.grad - Y.grad).abs().max()
+    Cr = C.double().clone().requires_grad_(True)
+    (scale * supcon_rows_reference(Cr, Cr, self_idx, key, key, temp, base).sum()).backward()
+    err = (X.grad.double() - Cr.grad).abs().max().item()
+    assert err < 1e-4 * Cr.grad.abs().max().item() + 1e-7, err
