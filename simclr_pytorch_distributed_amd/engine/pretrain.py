@@ -319,7 +319,11 @@ class PretrainEngine:
                 loss = loss + extra
         with ph("backward"):
             self.optimizer.zero_grad()
-            loss.backward()
+            # a persistent seed gradient: no ones-fill kernel per step
+            one = getattr(self, "_one_grad", None)
+            if one is None or one.device != loss.device or one.dtype != loss.dtype:
+                one = self._one_grad = torch.ones((), device=loss.device, dtype=loss.dtype)
+            loss.backward(one)
         if self.reducer is not None:
             with ph("grad_sync_wait"):
                 self.reducer.finish()
