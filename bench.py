@@ -140,6 +140,9 @@ def main():
             torch.cuda.synchronize()
         comm.barrier()
 
+    # --syncbn_comm auto (default) at N > 1: every candidate SyncBN transport is timed on real
+    # steps (state restored afterwards), ranks agree on the fastest; reported in the JSON line
+    tune = eng.autotune_syncbn(next_idx(0), steps=3, baseline=True) if n > 1 and not a.no_syncbn else None
     graphed = False
     if a.graph:
         # capture the whole step in one hipGraph (its 2 capture warm-up steps are real steps)
@@ -151,7 +154,9 @@ def main():
     for i in range(a.warmup):
         st0 = eng.train_step(next_idx(i), 1, i % iters, iters)
         if first_loss is None:
-            first_loss = st0["loss_local"]     # read after the timed region (no sync here)
+            # a snapshot (read after the timed region, no sync here): under --graph the stats
+            # dict is the captured graph's persistent output, overwritten by every replay
+            first_loss = st0["loss_local"].detach().clone()
     sync()
     # host cost of issuing one step into an idle queue (diagnostic, stderr)
     th = []
@@ -194,7 +199,9 @@ def main():
                        "global_batch": global_batch, "per_gpu_batch": per_gpu, "views": 2,
                        "image_size": size, "seq_len": None, "micro_batch_views": mb or None,
                        "parallelism": f"dp{n}" + ("+syncbn" if n > 1 and not a.no_syncbn else ""),
-                       "backend": eng.backend, "syncbn_transport": eng.syncbn_transport, "hip_graph": graphed,
+                       "backend": eng.backend, "syncbn_transport": eng.syncbn_transport,
+                       "syncbn_step_ms": tune["step_ms"] if tune else None,
+                       "syncbn_us_per_bn": tune.get("us_per_bn") if tune else None, "hip_graph": graphed,
                        "views_per_sec": round(2 * value, 2),
                        "peak_hbm_gb": round(peak_gb, 2), "hbm_capacity_gb": 288,
                        # first warm-up step and last timed step: the run trains from random init

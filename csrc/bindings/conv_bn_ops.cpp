@@ -49,15 +49,38 @@ void in_bn_ptrs(const OptT& sc, const OptT& sh, int64_t C, const float** ps, con
 // two-per-CU slots). The small 64x64 tile is only penalised when the GEMM is
 // compute-bound (long K); short-K (memory-bound) GEMMs favour its higher occupancy.
 // Calibrated with tools/conv_bench.py --cfg 0..3 on the ResNet-50 shapes.
-int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
-  // SDX_CONV_CFG=c pins the fwd/dgrad tile config (tests): the BN-statistics epilogue's per-tile
-  // fp32 partial sums then cover the same rows whatever the per-rank batch, so a W-rank step
-  // reproduces the single-rank statistics bit for bit (tests/test_gpu_dist.py)
+// SDX_CONV_CFG=c pins the fwd/dgrad tile config (tests): the BN-statistics epilogue's per-tile
+// fp32 partial sums then cover the same rows whatever the per-rank batch, so a W-rank step
+// reproduces the single-rank statistics bit for bit (tests/test_gpu_dist.py)
+int pinned_cfg() {
   static const int pinned = [] {
     const char* e = getenv("SDX_CONV_CFG");
-    return e != nullptr ? atoi(e) : -1;
+    const int v = e != nullptr ? atoi(e) : -1;
+    return v >= 0 && v <= 8 ? v : -1;
   }();
-  if (fill && pinned >= 0 && pinned <= 8) return pinned;
+  return pinned;
+}
+
+// fwd / dgrad tile config of a conv: the tap-reuse 3x3 loop where it applies (pad-1 stride-1
+// 3x3; not with a pinned config, the in-kernel statistics reduction or the BN+ReLU operand
+// prologue), else auto_cfg. SDX_TAP3: 0 never; 1 (default) where it measured faster than
+// the implicit-GEMM tiles — the single-chunk 256x64 tile (C = 64: layer 1) and 4x4 images
+// (layer 4), profiles/tap3_r5.txt; 2 every supported shape
+int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, bool plain) {
+  static const int tap = [] {
+    const char* e = getenv("SDX_TAP3");
+    return e == nullptr ? 1 : atoi(e);
+  }();
+  if (tap > 0 && plain && pinned_cfg() < 0) {
+    const int t = igemm_tap_cfg(g, cdim, ncol);
+    if (t >= 0 && (tap >= 2 || t == 11 || g.W == 4)) return t;
+  }
+  return auto_cfg(M, ncol, Kdim, true);
+}
+
+int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
+  const int pinned = pinned_cfg();
+  if (fill && pinned >= 0) return pinned;
   const int64_t bm[4] = {128, 256, 64, 64}, bn[4] = {128, 64, 256, 64};
   const bool long_k = Kdim == 0 || Kdim > 256;
   const double pen_long[4] = {1.0, 1.04, 1.04, 1.35}, pen_short[4] = {1.0, 1.0, 1.0, 1.05};
@@ -178,7 +201,8 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
   TORCH_CHECK(g.K % 8 == 0, "Cout must be a multiple of 8");
   c10::DeviceGuard dg(x.device());
   const int64_t M = (int64_t)g.N * g.P * g.Q;
-  if (cfg < 0) cfg = auto_cfg(M, g.K, (int64_t)g.R * g.S * g.C, true);
+  if (cfg < 0)
+    cfg = conv_cfg(g, g.C, g.K, M, (int64_t)g.R * g.S * g.C, fr == nullptr && !in_scale.has_value());
   TORCH_CHECK(!no_out || (want_stats && fr == nullptr && epi == nullptr), "statistics-only conv: stats, no epilogue");
   auto y = no_out ? torch::Tensor() : torch::empty({g.N, g.P, g.Q, g.K}, x.options());
   torch::Tensor slab;
@@ -254,7 +278,7 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
   c10::DeviceGuard dg(dy.device());
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = auto_cfg(M, g.C, (int64_t)g.R * g.S * g.K / (stride * stride), true);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), fr == nullptr);
   torch::Tensor dx;
   if (out.has_value()) {
     dx = *out;
@@ -383,7 +407,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   g.C = C; g.R = wt.size(1); g.S = wt.size(2);
   g.H = H; g.W = W; g.stride = stride; g.pad = pad;
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = auto_cfg(M, g.C, (int64_t)g.R * g.S * g.K / (stride * stride), true);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), fr == nullptr);
   int rows = 0;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) rows += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);

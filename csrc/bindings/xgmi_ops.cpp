@@ -153,6 +153,11 @@ int64_t xgmi_emu_create(int64_t world, int64_t cap, double timeout_s) {
   {
     const char* e = getenv("SDX_SYNCBN_EMU_SOLO");
     a->solo = e != nullptr && atoi(e) != 0;
+    // a timing diagnostic only (tools/syncbn_latency.py): the W-1 other slots are summed
+    // although no rank wrote them, so BN statistics of a training run are wrong under it
+    if (a->solo)
+      fprintf(stderr, "warning: SDX_SYNCBN_EMU_SOLO=1: emulated SyncBN runs one rank's share only "
+                      "(timing diagnostic; the BN statistics are NOT valid)\n");
   }
   check_hip(hipGetDevice(&a->device), "hipGetDevice");
   a->world = (int)world;

@@ -97,6 +97,9 @@ int igemm_tile_m(int cfg);
 int igemm_trace_slots();
 hipError_t igemm_trace_copy(unsigned long long* host, hipStream_t s);
 int igemm_tile_n(int cfg);
+// tap-reuse 3x3 tile config (11-13) for a pad-1 stride-1 3x3 conv whose reduction runs over
+// cdim channels and whose output has ncol channels (DGRAD: cdim = K, ncol = C), or -1
+int igemm_tap_cfg(const ConvGeom& g, int cdim, int ncol);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
 struct StatFuse;
 // sf (optional, with stats): reduce the statistics slab in-kernel (StatFuse)

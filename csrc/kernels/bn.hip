@@ -73,11 +73,16 @@ __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's data stores are acknowledged
   if (threadIdx.x == 0) ok = 1;
   __syncthreads();
-  if (threadIdx.x < W && !(XG == 2 && xg.solo && threadIdx.x != me)) {
-    // wave 0: the same wave that stored the data, after its drain
+  if (threadIdx.x < W) {
+    // wave 0: the same wave that stored the data, after its drain. Every lane p < W publishes
+    // this rank's flag to peer p; solo mode (one rank's share, diagnostic) then polls only
+    // its own slot (the other W-1 ranks count as already published)
     const int p = threadIdx.x;
     __hip_atomic_store(xg.peers.flags[p] + ((size_t)par * W + me) * kXgmiFlagGroups + blockIdx.x, xg.epoch,
                        __ATOMIC_RELAXED, kScope);
+  }
+  if (threadIdx.x < W && !(XG == 2 && xg.solo && threadIdx.x != me)) {
+    const int p = threadIdx.x;
     unsigned* f = xg.peers.flags[me] + ((size_t)par * W + p) * kXgmiFlagGroups + blockIdx.x;
     const long long t0 = wall_clock64();
     unsigned spins = 0;

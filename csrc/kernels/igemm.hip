@@ -145,7 +145,20 @@ struct IgemmParams {
   int ncls;
   Cls cls[4];
   FastDiv div_pq, div_q;   // WGRAD pixel decode
+  // DEPTH 7 / 8 (tap-reuse 3x3 fwd / stride-1 dgrad, launch_tap): the tile's input window —
+  // its image rows plus a pad row / column on each side, the "halo" — is staged ONCE per
+  // 64-channel chunk and all 9 taps read it at a uniform pixel offset. Halo pixel
+  // (img, hy, hx) is LDS row img·t_is + hy·t_rs + hx (t_rs = W + 2); its 16-B chunk q sits at
+  // q ^ ((hx + t_ky·hy) & 7), conflict-free fragment reads for every tap (see tap_halo_kb).
+  // t_hp halo pixels = t_nhp 1-KiB LDS-DMA pieces; t_nch channel chunks; the tile's first
+  // image row y0 within image n0.
+  int t_rs, t_is, t_ky, t_hp, t_nhp, t_nch, t_imgs;
 };
+
+// DEPTH 7 / 8 halo buffer size in KiB: the largest window a BM-row tile needs over the
+// supported image widths (BM = 256: 4 images of 8x8 = 4·10·10 pixels = 50 KiB at 64
+// channels; BM = 128: 8 images of 4x4 = 8·6·6 pixels = 36 KiB)
+constexpr int tap_halo_kb(int bm) { return bm == 256 ? 50 : 36; }
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -406,7 +419,11 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1, "4 or 8 waves");
   static_assert(T::A_CH >= 1 && T::B_CH >= 1, "tile too small for the thread count");
   constexpr int LDS_C = BM * (BN * 2 + 8);   // C-tile staging (epilogue)
-  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C) : (DEPTH >= 4 ? 3 : 2) * T::STAGE;
+  // DEPTH 7 / 8: 2 / 1 halo buffers, one junk KiB (LDS-DMA target of the unused halo issue
+  // slots), a 3-buffer ring of weight tiles
+  constexpr int LDS_TAP = (DEPTH == 7 ? 2 : 1) * tap_halo_kb(BM) * 1024 + 1024 + 3 * T::B_BYTES;
+  constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C)
+                          : DEPTH >= 7 ? LDS_TAP : (DEPTH >= 4 ? 3 : 2) * T::STAGE;
   static_assert(!ONE || DEPTH == 3, "single-stage variant is LDS-DMA only");
   static_assert(DEPTH < 4 || MODE != MODE_WGRAD, "LDS-DMA ring is FWD/DGRAD only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
@@ -1012,7 +1029,198 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
   // are issued while tile k computes and the LDS write of tile k+1 waits only for loads
   // issued a whole K-tile earlier (load latency covered by two tiles of MFMA work).
-  if constexpr (DEPTH == 6) {
+  if constexpr (DEPTH == 7 || DEPTH == 8) {
+    // Tap-reuse 3x3 (stride 1, pad 1) loop. The implicit GEMM above re-gathers a shifted copy
+    // of the A tile for every tap (9 LDS-DMA fills of BM rows per 64 channels, the per-CU fill
+    // bandwidth sets the pace: profiles/conv_core_r4.txt). Here the tile's input window (the
+    // halo: its image rows plus the pad ring) is staged ONCE per 64-channel chunk and each of
+    // the 9 taps is a step that reads it at a uniform pixel offset; only the weight tile
+    // (BN x 64, L2-resident) is staged per step, through a 3-buffer ring. The step structure
+    // is DEPTH 6's: step-1 fragments read under step-0 MFMAs, ONE raw barrier per step, then
+    // the freed weight buffer is refilled with step s+3 and step-0 fragments of s+1 are read,
+    // interleaved with step-1 MFMAs. DEPTH 7 double-buffers the halo: chunk c+1's window is
+    // issued one 1-KiB piece per step during chunk c (a wave has at most 8 pieces; the 9th slot
+    // and unused ones DMA the zero page into a junk KiB, so every step issues exactly NL DMAs
+    // and one counted vmcnt covers them). DEPTH 8: a single chunk (C = 64), one halo buffer.
+    // RAW: a weight tile / halo piece issued in iteration i is retired by the vmcnt(NL) of
+    // iteration i+2 (the NL youngest are iteration i+1's), before that iteration's barrier;
+    // chunk c+1's pieces go out in iterations 9c-1 .. 9c+6 and are first read after the
+    // barrier of iteration 9c+8. WAR: the weight buffer of step s is refilled after the
+    // barrier that follows its last reads; halo buffer (c+1)&1 held chunk c-1, last read
+    // before the barrier of iteration 9c-1, refilled from after that barrier on.
+    constexpr int NW = NT / 64;
+    constexpr int NHB = DEPTH == 7 ? 2 : 1;
+    constexpr int HKB = tap_halo_kb(BM);
+    constexpr int NHW = (HKB + NW - 1) / NW;    // halo pieces per wave per chunk (max)
+    static_assert(DEPTH == 8 || NHW <= 8, "a chunk's halo pieces must be issued within 8 steps");
+    constexpr int NL = T::B_CH + (DEPTH == 7 ? 1 : 0);   // LDS-DMAs per wave per step
+    unsigned char* const junk = smem + NHB * HKB * 1024;
+    unsigned char* const bring = junk + 1024;
+    const int HW = g.H * g.W;
+    const int nimg0 = m0 / HW;
+    const int y0 = p.t_imgs > 0 ? 0 : (m0 - nimg0 * HW) / g.W;   // t_imgs 0: a band of one image
+    const int nch = p.t_nch;
+    const int nk7 = 9 * nch;
+    // halo pieces of this wave: piece wvu + NW·i; lane L carries pixel 8·piece + L/8, physical
+    // chunk L%8 = logical chunk (L%8) ^ swizzle. Source element (chunk 0) or -1 (zero: pad ring,
+    // images past N, pixels past the window)
+    // (9 slots: the in-loop halo slot of the step with tap j uses slot 0 and then rotates the
+    // slots by one, so slot 0 always holds piece j's source without a dynamic index, which
+    // hipcc would serve from scratch)
+    // (DEPTH 8 issues all its pieces in the prologue only: NHW may exceed 9 there)
+    int hsrc[NHW > 9 ? NHW : 9];
+#pragma unroll
+    for (int i = NHW; i < 9; ++i) hsrc[i] = -1;
+#pragma unroll
+    for (int i = 0; i < NHW; ++i) {
+      const int P = (wvu + NW * i) * 8 + (lane >> 3);
+      const int img = P / p.t_is, rem = P - img * p.t_is;
+      const int hy = rem / p.t_rs, hx = rem - hy * p.t_rs;
+      const int n = nimg0 + img, yin = y0 - 1 + hy, xin = hx - 1;
+      const int q = (lane & 7) ^ ((hx + p.t_ky * hy) & 7);
+      const bool ok = P < p.t_hp && n < g.N && (unsigned)yin < (unsigned)g.H && (unsigned)xin < (unsigned)g.W;
+      SDX_DCHECK(!ok || (long)((n * g.H + yin) * g.W + xin) * cdim + nch * 64 <= p.a_elems);
+      hsrc[i] = ok ? ((n * g.H + yin) * g.W + xin) * cdim + q * 8 : -1;
+    }
+    auto halo_piece = [&](int i, int src, int ch, int hbuf, bool real) {
+      const int pc = wvu + NW * i;
+      real = real && pc < p.t_nhp;
+      unsigned char* dst = real ? smem + hbuf * (HKB * 1024) + pc * 1024 : junk;
+      const gptr16 s = (real && src >= 0) ? (gptr16)(p.a + src + ch * 64) : zp;
+      glds16(s, dst);
+    };
+    // A fragment rows: za = (halo row of the lane's output pixel at tap (0, 0))·128 + its
+    // swizzle phase; a tap adds a uniform (row offset·128 + phase offset)
+    int za[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WTM + 16 * i + c;
+      int img, y, x;
+      if (p.t_imgs > 0) {
+        img = ml / HW;
+        const int rem = ml - img * HW;
+        y = rem / g.W;
+        x = rem - y * g.W;
+      } else {
+        img = 0;
+        y = ml / g.W;
+        x = ml - y * g.W;
+      }
+      za[i] = (img * p.t_is + y * p.t_rs + x) * 128 + ((x + p.t_ky * y) & 7);
+    }
+    // uniform part of a step's A address: halo buffer + tap (FWD reads input row y + r − 1 =
+    // halo row y + r; DGRAD reads dy row y + 1 − r = halo row y + 2 − r)
+    auto hoff = [&](int r, int s, int ch) {
+      const int rr = MODE == MODE_FWD ? r : 2 - r, ss = MODE == MODE_FWD ? s : 2 - s;
+      return (NHB == 2 ? (ch & 1) * (HKB * 1024) : 0) + (rr * p.t_rs + ss) * 128 + ss + p.t_ky * rr;
+    };
+    auto read_a7 = [&](int ho, int u, bf16x8 (&af)[TM]) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int w = za[i] + ho;
+        const int a = (w & ~127) | ((((w & 7) ^ (4 * u + h))) << 4);
+        af[i] = *reinterpret_cast<const bf16x8*>(smem + a);
+      }
+    };
+    auto read_b7 = [&](int bb, int u, bf16x8 (&bfr)[TN]) {
+      const unsigned char* sb = bring + bb * T::B_BYTES;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag_kin(sb, wn * WTN + 16 * j + c, u);
+    };
+    // weight tile of step (r, s, ch) into ring buffer bb (past the last step: the zero page)
+    auto issue_b7 = [&](int r, int s, int ch, int bb) {
+      const bool kok = ch < nch;
+      const int kb = p.b_t0 + r * p.b_tr + s * p.b_ts + ch * 64 + kin_ch * 8;
+#pragma unroll
+      for (int i = 0; i < T::B_CH; ++i) {
+        const bool ok = kok && b_off[i] >= 0;
+        SDX_DCHECK(!ok || (long)b_off[i] + kb + 8 <= p.b_elems);
+        const gptr16 src = ok ? (gptr16)(p.b + b_off[i] + kb) : zp;
+        glds16(src, bring + bb * T::B_BYTES + 8 * (wvu * T::B_CH + i) * BK * 2);
+      }
+    };
+    // the halo slot of the iteration that reads step (rc, sc, cc): piece 3·rc + sc of chunk cc+1
+    auto halo_slot = [&](int rc, int sc, int cc) {
+      if constexpr (DEPTH == 7) {
+        const int j = 3 * rc + sc;
+        halo_piece(j, hsrc[0], cc + 1, (cc + 1) & 1, j < NHW && cc + 1 < nch);
+        const int t = hsrc[0];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) hsrc[q] = hsrc[q + 1];
+        hsrc[8] = t;
+      }
+    };
+    auto adv = [](int& r, int& s, int& ch) {
+      s += 1;
+      const bool w1 = s == 3;
+      s = w1 ? 0 : s;
+      r += w1 ? 1 : 0;
+      const bool w2 = r == 3;
+      r = w2 ? 0 : r;
+      ch += w2 ? 1 : 0;
+    };
+    // prologue: chunk 0's window, the weight tiles of steps 0-2 (+ the halo slots of
+    // iterations -3, -2 (none) and -1 (piece 0 of chunk 1))
+#pragma unroll
+    for (int i = 0; i < NHW; ++i) halo_piece(i, hsrc[i], 0, 0, true);
+    int ir = 0, is = 0, ic = 0;   // weight-issue step
+    issue_b7(ir, is, ic, 0);
+    adv(ir, is, ic);
+    if constexpr (DEPTH == 7) halo_piece(0, 0, 0, 0, false);
+    issue_b7(ir, is, ic, 1);
+    adv(ir, is, ic);
+    if constexpr (DEPTH == 7) halo_piece(0, 0, 0, 0, false);
+    issue_b7(ir, is, ic, 2);
+    adv(ir, is, ic);
+    halo_slot(0, 0, 0);
+    vm_wait<2 * NL>();   // chunk 0's window and step 0's weights landed
+    lds_barrier();
+    stamp(1);
+    bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+    int cr = 0, cs = 0, cc = 0, rb = 0;   // read step, its weight buffer
+    read_a7(hoff(0, 0, 0), 0, a0);
+    read_b7(0, 0, b0);
+    for (int kt = 0; kt < nk7; ++kt) {
+      if (!(SDX_W1_ABL && (p.ablate & 8))) {
+        read_a7(hoff(cr, cs, cc), 1, a1);
+        read_b7(rb, 1, b1);
+      }
+      if (!(SDX_W1_ABL && (p.ablate & 4))) mfma_u(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt < 160) stamp(2 + 3 * kt);
+      vm_wait<NL>();
+      lds_barrier();
+      if (kt < 160) stamp(3 + 3 * kt);
+      const int fb = rb;
+      adv(cr, cs, cc);
+      rb = rb == 2 ? 0 : rb + 1;
+      // step kt+1 (at kt = nk7-1 a harmless read inside the LDS image, never used)
+      if (!(SDX_W1_ABL && (p.ablate & 8))) {
+        read_a7(hoff(cr, cs, NHB == 2 ? cc : 0), 0, a0);
+        read_b7(rb, 0, b0);
+      }
+      if (!(SDX_W1_ABL && (p.ablate & 2))) {
+        issue_b7(ir, is, ic, fb);
+        halo_slot(cr, cs, cc);
+      } else {
+        // timing ablation: keep the per-step DMA count (the counted vmcnt) with zero-page DMAs
+#pragma unroll
+        for (int i = 0; i < NL; ++i) glds16(zp, junk);
+      }
+      adv(ir, is, ic);
+      if (!(SDX_W1_ABL && (p.ablate & 4))) mfma_u(a1, b1);
+      if constexpr (SDX_W1_SGB) static_for<0, TM * TN>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // up to 5 VALU
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // up to 1 VMEM read (LDS-DMA)
+        __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);   // up to 2 SALU
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the zero-page DMAs past the end must land before any wave's epilogue reuses the LDS
+    vm_wait<0>();
+    __syncthreads();
+  } else if constexpr (DEPTH == 6) {
     // One wave per SIMD (4-wave block, 64x128 / 128x64 wave tiles: half the LDS fragment
     // bytes per MFMA of the 8-wave 64x32 tiles) over a 3-buffer LDS-DMA ring, pipelined
     // inside each wave. A K-tile is two 32-deep k-steps: the fragments of step 1 are read
@@ -1675,7 +1883,7 @@ template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   // LDS-DMA main loops (DEPTH 3: two buffers; 5: ping-pong ring) carry every epilogue
   // variant; the single-stage (ONE) form is DEPTH 3 at one K-tile
-  constexpr bool GLK = (DEPTH == 3 || DEPTH == 5 || DEPTH == 6) && MODE != MODE_WGRAD;
+  constexpr bool GLK = (DEPTH == 3 || DEPTH >= 5) && MODE != MODE_WGRAD;
   const bool one = DEPTH == 3 && p.Kdim <= BK && igemm_one();
   if (MODE == MODE_FWD && p.bn_sc != nullptr) {
     // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
@@ -1802,6 +2010,46 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   }
 }
 
+// Geometry of the tap-reuse loop (DEPTH 7 / 8) for a BM-row tile; false = not supported:
+// a pad-1 3x3 stride-1 conv (DGRAD: the stride-1 class) whose tile rows are whole image
+// rows of whole images or of one image band, a channel dim of 64-channel chunks and a window
+// that fits the halo buffer. Swizzle phase t_ky: fragments of 16 output pixels span 1 row
+// (W >= 16), 2 rows (W = 8: ky = 0) or 4 rows (W = 4: ky = 4) — conflict-free ds_read_b128
+// lane groups for every tap (checked by brute force over the lane groups of the LDS table in
+// MI355X_MICROARCH.md); other widths are correct, not conflict-free.
+bool tap_geom(IgemmParams& p, int bm, int depth, int mode) {
+  const ConvGeom& g = p.g;
+  if (g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || g.P != g.H || g.Q != g.W) return false;
+  if (mode == MODE_DGRAD && (p.ncls > 1 || p.ph != 0 || p.pw != 0 || p.nr != 3 || p.ns != 3)) return false;
+  const int cdim = mode == MODE_FWD ? g.C : g.K;
+  const int HW = g.H * g.W;
+  if (cdim % 64 != 0 || bm % g.W != 0 || !(HW % bm == 0 || bm % HW == 0)) return false;
+  p.t_rs = g.W + 2;
+  p.t_imgs = bm >= HW ? bm / HW : 0;
+  const int rows = bm >= HW ? g.H : bm / g.W;
+  p.t_is = (rows + 2) * p.t_rs;
+  p.t_hp = (p.t_imgs > 0 ? p.t_imgs : 1) * p.t_is;
+  p.t_nhp = (p.t_hp + 7) / 8;
+  p.t_ky = g.W == 4 ? 4 : 0;
+  p.t_nch = cdim / 64;
+  if (p.t_nhp > tap_halo_kb(bm)) return false;
+  if (depth == 8 && p.t_nch != 1) return false;
+  return true;
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
+hipError_t launch_tap(IgemmParams p, hipStream_t s) {
+  if (!tap_geom(p, BM, DEPTH, MODE)) return hipErrorInvalidValue;
+  // the in-kernel statistics reduction and the BN+ReLU operand prologue are not built here
+  if (p.sf.cnt != nullptr || p.in_scale != nullptr) return hipErrorInvalidValue;
+  p.ablate = igemm_ablate();
+  p.trace = igemm_trace_on();
+  p.m_tiles = (p.M + BM - 1) / BM;
+  p.n_tiles = (p.Ncol + BN - 1) / BN;
+  const bool bs = MODE == MODE_DGRAD && p.bs.slab != nullptr;
+  return launch_k<MODE, BM, BN, WM, WN, DEPTH>(bs, p.m_tiles * p.n_tiles, p, s);
+}
+
 // tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
 // 4 128x128 with 8 waves (2x4 of 64x32: twice the waves per SIMD for latency hiding),
 // 5 256x128 with 8 waves (4x2 of 64x64, one block per CU), 6 128x256 with 8 waves (2x4 of
@@ -1820,6 +2068,18 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
     case 6: return launch_cfg<MODE, 128, 256, 2, 4>(p, s);
     case 7: return launch_cfg<MODE, 128, 256, 2, 2>(p, s);
     case 8: return launch_cfg<MODE, 256, 128, 2, 2>(p, s);
+    // tap-reuse 3x3 (FWD / stride-1 DGRAD only): 11 256x64 with 4 waves of 64x64 and one halo
+    // buffer (C = 64: two blocks per CU), 12 256x128 with 8 waves (4x2 of 64x64), 13 128x128
+    // with 8 waves (2x4 of 64x32)
+    case 11:
+      if constexpr (MODE != MODE_WGRAD) return launch_tap<MODE, 256, 64, 4, 1, 8>(p, s);
+      return hipErrorInvalidValue;
+    case 12:
+      if constexpr (MODE != MODE_WGRAD) return launch_tap<MODE, 256, 128, 4, 2, 7>(p, s);
+      return hipErrorInvalidValue;
+    case 13:
+      if constexpr (MODE != MODE_WGRAD) return launch_tap<MODE, 128, 128, 2, 4, 7>(p, s);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -1827,12 +2087,26 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
 }  // namespace
 
 int igemm_tile_m(int cfg) {
-  static const int m[9] = {128, 256, 64, 64, 128, 256, 128, 128, 256};
-  return m[cfg];
+  static const int m[14] = {128, 256, 64, 64, 128, 256, 128, 128, 256, 0, 0, 256, 256, 128};
+  return (cfg >= 0 && cfg < 14) ? m[cfg] : 0;
 }
 int igemm_tile_n(int cfg) {
-  static const int n[9] = {128, 64, 256, 64, 128, 128, 256, 256, 128};
-  return n[cfg];
+  static const int n[14] = {128, 64, 256, 64, 128, 128, 256, 256, 128, 0, 0, 64, 128, 128};
+  return (cfg >= 0 && cfg < 14) ? n[cfg] : 0;
+}
+
+// tap-reuse tile config for a conv (FWD, or the stride-1 DGRAD with cdim = K, ncol = C), or -1
+int igemm_tap_cfg(const ConvGeom& g, int cdim, int ncol) {
+  if (g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || cdim % 64 != 0) return -1;
+  const int cands[3] = {cdim == 64 && ncol <= 64 ? 11 : -1, g.W >= 8 ? 12 : -1, 13};
+  for (int cfg : cands) {
+    if (cfg < 0) continue;
+    IgemmParams p{};
+    p.g = g;
+    p.g.C = cdim;   // checked as a FWD geometry whose reduction channels are cdim
+    if (tap_geom(p, igemm_tile_m(cfg), cfg == 11 ? 8 : 7, MODE_FWD)) return cfg;
+  }
+  return -1;
 }
 
 namespace {
@@ -2141,7 +2415,11 @@ hipError_t splitk_flush() {
 
 hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float* dw, int accumulate, hipStream_t s) {
   if (splitk_deferring(s)) {
-    if (g_jobs.n == kMaxSplitkJobs) {
+    // the queued jobs run unordered in one launch: a second job into the same sink would race
+    // its read-modify-write with the first (a shared or tied weight) — issue the queue first
+    bool dup = false;
+    for (int i = 0; i < g_jobs.n; ++i) dup = dup || g_jobs.dw[i] == dw;
+    if (g_jobs.n == kMaxSplitkJobs || dup) {
       // queue full: issue what is queued and keep deferring
       hipStream_t keep = g_defer_stream;
       const hipError_t e = splitk_flush();

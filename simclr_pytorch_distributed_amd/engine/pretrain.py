@@ -186,43 +186,125 @@ class PretrainEngine:
     syncbn_transport = "none"
 
     def _setup_syncbn_comm(self, opt, dev):
-        """SyncBN statistics transport for the native backend.
+        """SyncBN statistics transport for the native backend (SURVEY §2.3 X4/X6, §5.8;
+        reference: main_supcon.py:222-224 converts the model to SyncBatchNorm).
 
-        ``--syncbn_comm auto`` / ``xgmi`` (opt-in): the one-shot IPC arena, whose FUSED
-        path reduces, exchanges and finalizes every BN's statistics in one launch
-        (parallel/xgmi.py); ``auto`` uses it whenever all ranks are peers on one node and
-        falls back to RCCL otherwise. ``rccl`` (default): a dedicated RCCL communicator. Either is
-        registered as a native handle, so the C++ block executor exchanges each BN's sums
-        itself on the compute stream. gloo (CPU tests, shared-GPU tests) keeps the Python
-        collective path."""
-        want = getattr(opt, "syncbn_comm", "rccl")
+        Candidates, each registered as a native handle so the C++ block executor exchanges
+        each BN's sums itself on the compute stream:
+
+        * ``xgmi-fused``: the one-shot IPC arena whose FUSED path reduces, exchanges and
+          finalizes a BN's statistics in ONE launch (parallel/xgmi.py); all ranks must be
+          peers on one node.
+        * ``rccl-native``: a dedicated RCCL communicator (reduce -> ncclAllReduce ->
+          finalize per BN).
+        * ``process-group``: no native handle; the Python collective path (gloo runs).
+
+        ``--syncbn_comm auto`` (default) sets up every candidate the job can have and MEASURES
+        them on the first training batch (:meth:`autotune_syncbn`): all ranks agree on the
+        fastest one (timings MAX-reduced over ranks, so the choice is identical everywhere).
+        ``xgmi`` / ``rccl`` force one (RCCL is the fallback of both when the arena's self-check
+        fails)."""
+        want = getattr(opt, "syncbn_comm", "auto")
+        self._syncbn_cands = {}
         if dev.type != "cuda":
             return
         timeout = float(getattr(opt, "comm_timeout", 600.0))
         if want in ("xgmi", "auto"):
             # set-up is agreed step by step across ranks (parallel/xgmi.py): either every
-            # rank gets the arena or every rank raises here and falls back to RCCL together
+            # rank gets the arena or every rank raises here and falls back together
             try:
                 from ..parallel.xgmi import OneShotAllReduce
                 impl = OneShotAllReduce(timeout_s=timeout)
                 self._xgmi = impl
-                comm.set_small_allreduce(None, impl)
-                comm.set_native_small_comm(None, impl.handle)
-                self.syncbn_transport = "xgmi-fused"
-                logging.info("SyncBN statistics: fused one-shot xGMI exchange (native executor)")
-                return
+                self._syncbn_cands["xgmi-fused"] = (impl.handle, impl)
             except Exception as e:  # noqa: BLE001
                 (logging.warning if want == "xgmi" else logging.info)(
                     f"one-shot xGMI exchange unavailable ({e}); using RCCL")
-        if comm.backend() == "nccl" and os.environ.get("SDX_NATIVE_SYNCBN", "1") != "0":
+        if (want == "auto" or not self._syncbn_cands) and comm.backend() == "nccl" \
+                and os.environ.get("SDX_NATIVE_SYNCBN", "1") != "0":
             # 0 on every rank together when the dedicated communicator cannot be set up
             handle = comm.create_rccl_small_comm(None, timeout)
             if handle:
-                comm.set_native_small_comm(None, handle)
-                self.syncbn_transport = "rccl-native"
-                logging.info("SyncBN statistics: dedicated RCCL communicator (native executor)")
+                self._syncbn_cands["rccl-native"] = (handle, None)
+        if want == "auto" and comm.backend() != "nccl":
+            self._syncbn_cands["process-group"] = (0, None)
+        if not self._syncbn_cands:
+            logging.warning("SyncBN statistics use the process-group all-reduce")
+            return
+        # until the measurement: RCCL when present (the conservative transport), else the first
+        first = "rccl-native" if "rccl-native" in self._syncbn_cands else next(iter(self._syncbn_cands))
+        self._activate_syncbn(first)
+        self._syncbn_pending = want == "auto" and len(self._syncbn_cands) > 1
+        logging.info(f"SyncBN statistics: {first} (candidates {list(self._syncbn_cands)})")
+
+    _syncbn_cands: dict = {}
+    _syncbn_pending = False
+    syncbn_tune: Optional[dict] = None
+
+    def _activate_syncbn(self, name: str):
+        handle, impl = self._syncbn_cands[name]
+        comm.set_small_allreduce(None, impl)
+        comm.set_native_small_comm(None, handle)
+        self.syncbn_transport = name
+
+    def autotune_syncbn(self, idx: torch.Tensor, steps: int = 3, baseline: bool = False) -> Optional[dict]:
+        """Pick the SyncBN transport by timing real training steps on batch ``idx`` with each
+        candidate (one untimed step each first). The training state the steps touch
+        (parameters, optimizer and BN buffers, the norm EMA) is restored afterwards, so the
+        run follows the trajectory it would have had. Every rank measures its own step
+        time; the times are MAX-reduced over the ranks (the step is as slow as its slowest
+        rank) and every rank takes the argmin of the SAME reduced vector, so the choice is
+        identical everywhere. ``baseline``: also time the step with rank-local BN statistics
+        (no exchange, timing only) to report each transport's cost per exchanged BN.
+        SDX_SYNCBN_TUNE_SKEW="rank:name:ms[,...]" adds ms to a rank's measurement (tests)."""
+        self._syncbn_pending = False
+        names = list(self._syncbn_cands)
+        if self.device.type != "cuda" or (len(names) < 2 and not baseline) or not names:
+            return None
+        if baseline:
+            names = names + ["local-bn"]
+        state = [self.flat.flat, self.optimizer.buf, self.record_norm_mean, self._rnm_valid]
+        state += [t for t in self.model.buffers()]
+        if getattr(self.optimizer, "norms", None) is not None:
+            state.append(self.optimizer.norms)
+        snap = [t.detach().clone() for t in state]
+        active = self.syncbn_transport
+        group = self.runner.sync_group
+        self._host_prelude(1, 0, 1)
+        ms = []
+        for nm in names:
+            if nm == "local-bn":
+                self.runner.sync_group = None
             else:
-                logging.warning("SyncBN statistics use the process-group all-reduce")
+                self._activate_syncbn(nm)
+            self._step_body(idx)
+            torch.cuda.synchronize()
+            comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                self._step_body(idx)
+            torch.cuda.synchronize()
+            comm.barrier()
+            ms.append((time.perf_counter() - t0) / steps * 1e3)
+            self.runner.sync_group = group
+        with torch.no_grad():
+            for t, v in zip(state, snap):
+                t.copy_(v)
+        for item in filter(None, os.environ.get("SDX_SYNCBN_TUNE_SKEW", "").split(",")):
+            r, nm, extra = item.split(":")
+            if int(r) == self.rank and nm in names:
+                ms[names.index(nm)] += float(extra)
+        real = [i for i, nm in enumerate(names) if nm != "local-bn"]
+        best, red = comm.agree_fastest(names, ms, eligible=real)
+        self._activate_syncbn(best if best in self._syncbn_cands else active)
+        n_bn = 2 * sum(1 for mod in self.model.encoder.modules() if isinstance(mod, torch.nn.BatchNorm2d))
+        self.syncbn_tune = {"chosen": best, "step_ms": {nm: round(v, 3) for nm, v in zip(names, red)},
+                            "exchanges_per_step": n_bn}
+        if baseline:
+            base = red[names.index("local-bn")]
+            self.syncbn_tune["us_per_bn"] = {names[i]: round((red[i] - base) * 1e3 / n_bn, 2) for i in real}
+        logging.info(f"SyncBN transport measured: {self.syncbn_tune}")
+        return self.syncbn_tune
 
     def _setup_gather_comm(self, opt, dev):
         """Native transport of the contrastive loss's embedding all-gather / reduce-scatter
@@ -510,6 +592,9 @@ class PretrainEngine:
         for it, idx in enumerate(self.sampler.batches(self.device)):
             if it >= iters:
                 break
+            if self._syncbn_pending:
+                # --syncbn_comm auto: measure the transports on this batch (state restored)
+                self.autotune_syncbn(idx)
             data_time.update(time.time() - end)
             if opt.cuda_graph and self._graph is None and not getattr(self, "_graph_failed", False):
                 try:

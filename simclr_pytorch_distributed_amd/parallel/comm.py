@@ -216,6 +216,20 @@ def agree(ok: bool, group=None) -> bool:
     return bool(int(t.item()))
 
 
+def agree_fastest(names, times, eligible=None, group=None):
+    """All ranks pick the same option from per-rank timings: ``times[i]`` (this rank's
+    measurement of ``names[i]``) is MAX-reduced over the ranks — an option is as slow as its
+    slowest rank — and every rank takes the argmin over ``eligible`` indices (default all) of
+    the SAME reduced vector (ties: the first). Returns (name, reduced times)."""
+    t = torch.tensor([float(v) for v in times], dtype=torch.float64, device=_agree_device(group)
+                     if is_dist() else torch.device("cpu"))
+    if is_dist():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    red = t.tolist()
+    idx = list(range(len(names))) if eligible is None else list(eligible)
+    return names[min(idx, key=lambda i: (red[i], i))], red
+
+
 def negotiate(steps, cleanup, group=None):
     """Run a multi-step set-up in which ranks must stay in lock-step.
 

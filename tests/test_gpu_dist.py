@@ -21,14 +21,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _launch(world, out, syncbn_comm="", model="resnet18", compress="", steps=1):
+def _launch(world, out, syncbn_comm="", model="resnet18", compress="", steps=1, pin=True):
     # file-store rendezvous: no probed TCP port that another job on the box can take first
     rdv = os.path.join(str(out), f"rdv_{model}_{world}_{syncbn_comm or 'pg'}{compress}")
     procs = []
     for r in range(world):
         env = dict(os.environ, SDX_TEST_SYNCBN_COMM=syncbn_comm, SDX_TEST_MODEL=model, RANK=str(r), LOCAL_RANK="0",
                    SDX_TEST_GRAD_COMPRESS=compress, SDX_TEST_STEPS=str(steps),
-                   WORLD_SIZE=str(world), SDX_CONV_CFG="4",
+                   WORLD_SIZE=str(world), SDX_CONV_CFG="4" if pin else "-1",
                    MASTER_ADDR="127.0.0.1", SDX_INIT_METHOD="file://" + rdv, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -134,3 +134,55 @@ def test_four_rank_resnet50_fused_syncbn_three_steps(gpu, tmp_path):
     assert abs(sum(d["loss"] for d in ranks) - ref["loss"]) < 1e-2 * abs(ref["loss"]) + 1e-3
     assert med < 2e-2, med
     assert worst[0][0] < 6e-2, worst[:8]
+
+
+def test_four_rank_resnet50_unpinned_replicas(gpu, tmp_path):
+    """The W=4 three-step run with the PRODUCTION tile selection (no SDX_CONV_CFG pin: the
+    tap-reuse 3x3 loop, the in-wave pipelined DEPTH 6 tiles, auto configs at the per-rank
+    batch): the replicas' parameters and BN running statistics stay bit-identical across the
+    four ranks after every step (fused xGMI SyncBN arena, gloo process group)."""
+    _launch(4, tmp_path, "xgmi", "resnet50", steps=3, pin=False)
+    ranks = [torch.load(tmp_path / f"resnet50_w4_r{r}.pt", weights_only=True) for r in range(4)]
+    a = ranks[0]
+    assert len(a["hashes"]) == 3
+    for d in ranks[1:]:
+        assert torch.equal(d["grad"], a["grad"]), "all-reduced step-1 gradients differ across ranks"
+        assert d["hashes"] == a["hashes"], (d["hashes"], a["hashes"])
+
+
+def test_syncbn_autotune_agrees(gpu, tmp_path):
+    """--syncbn_comm auto at W=2 (gloo process group on one GPU: candidates = the fused xGMI
+    arena and the process-group path): every rank ends on the SAME transport, also when one
+    rank's measurement of the faster transport is skewed (SDX_SYNCBN_TUNE_SKEW); the timing
+    steps leave the training state untouched; the per-BN cost is reported against the
+    local-BN baseline (engine/pretrain.py autotune_syncbn, bench.py syncbn_* fields)."""
+    import json
+    for skew in ("", "1:xgmi-fused:100000,1:process-group:0"):
+        d = tmp_path / ("skew" if skew else "plain")
+        d.mkdir()
+        procs = []
+        for r in range(2):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                       SDX_INIT_METHOD="file://" + str(d / "rdv"), PYTHONPATH=ROOT, OMP_NUM_THREADS="4",
+                       SDX_SYNCBN_TUNE_SKEW=skew)
+            procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_gpu_tune_worker.py"),
+                                           str(d)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                          text=True))
+        for p in procs:
+            try:
+                _, err = p.communicate(timeout=300)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                pytest.fail("tune worker timed out")
+            assert p.returncode == 0, err[-3000:]
+        res = [json.load(open(d / f"tune_r{r}.json")) for r in range(2)]
+        print(skew or "no skew", res[0]["tune"])
+        assert res[0]["tune"] is not None and set(res[0]["tune"]["step_ms"]) == {"xgmi-fused", "process-group",
+                                                                                   "local-bn"}
+        assert res[0]["transport"] == res[1]["transport"] == res[0]["tune"]["chosen"]
+        assert res[0]["tune"] == res[1]["tune"]
+        assert all(x["restored"] for x in res)
+        assert set(res[0]["tune"]["us_per_bn"]) == {"xgmi-fused", "process-group"}
+        if skew:
+            assert res[0]["transport"] == "process-group"

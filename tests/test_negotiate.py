@@ -73,3 +73,43 @@ def test_negotiate_lockstep(world, fail_rank, fail_step):
         assert log.endswith("cleanup"), (r, log)
         assert f"enter{fail_step + 1}" not in log, (r, log)     # nobody went on alone
         assert (err == "RuntimeError") == (r == fail_rank), (r, err)
+
+
+def _fastest_entry(rank, world, port, d):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        from simclr_pytorch_distributed_amd.parallel import comm
+        names = ["xgmi-fused", "rccl-native", "local-bn"]
+        # every rank measures xgmi faster, except rank world-1 (timing skew: a slow peer);
+        # local-bn is the fastest everywhere but not eligible (a timing baseline only)
+        ms = [10.0 + 0.1 * rank, 11.0, 5.0]
+        if rank == world - 1:
+            ms[0] = 13.0
+        best, red = comm.agree_fastest(names, ms, eligible=[0, 1])
+        with open(os.path.join(d, f"f{rank}.txt"), "w") as f:
+            f.write(best + " " + ",".join(f"{v:.3f}" for v in red))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_agree_fastest_transport_under_skew(world):
+    """SyncBN transport choice (engine/pretrain.py autotune_syncbn): per-rank timings that
+    disagree (one slow rank) still give ONE choice on every rank — the option whose slowest
+    rank is fastest — and an ineligible baseline is never chosen."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_fastest_entry, args=(world, port, d), nprocs=world, join=True)
+        res = [open(os.path.join(d, f"f{r}.txt")).read().split(" ") for r in range(world)]
+    assert {b for b, _ in res} == {"rccl-native"}
+    assert len({t for _, t in res}) == 1      # the same reduced vector everywhere
+    assert res[0][1].split(",")[0] == "13.000"
+
+
+def test_agree_fastest_single_process():
+    from simclr_pytorch_distributed_amd.parallel import comm
+    best, red = comm.agree_fastest(["a", "b", "c"], [3.0, 2.0, 2.0])
+    assert best == "b" and red == [3.0, 2.0, 2.0]
