@@ -63,9 +63,10 @@ int pinned_cfg() {
 
 // fwd / dgrad tile config of a conv: the tap-reuse 3x3 loop where it applies (pad-1 stride-1
 // 3x3; not with a pinned config, the in-kernel statistics reduction or the BN+ReLU operand
-// prologue), else auto_cfg. SDX_TAP3: 0 never; 1 (default) where it measured faster than
-// the implicit-GEMM tiles — the single-chunk 256x64 tile (C = 64: layer 1) and 4x4 images
-// (layer 4), profiles/tap3_r5.txt; 2 every supported shape
+// prologue), else auto_cfg. SDX_TAP3=0 disables it. Per shape (tools/tap3_sweep.py,
+// profiles/tap3_r5.txt) it beats the best implicit-GEMM tile at every CIFAR ResNet-50 3x3:
+// fwd / dgrad l1 52 / 51 vs 67 / 68 us, l2 45 / 42 vs 47 / 45, l3 34 / 34 vs 38 / 37,
+// l4 38 / 38 vs 58 / 56
 int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, bool plain) {
   static const int tap = [] {
     const char* e = getenv("SDX_TAP3");
@@ -73,7 +74,7 @@ int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, boo
   }();
   if (tap > 0 && plain && pinned_cfg() < 0) {
     const int t = igemm_tap_cfg(g, cdim, ncol);
-    if (t >= 0 && (tap >= 2 || t == 11 || g.W == 4)) return t;
+    if (t >= 0) return t;
   }
   return auto_cfg(M, ncol, Kdim, true);
 }

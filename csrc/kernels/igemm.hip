@@ -1038,39 +1038,40 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     // (BN x 64, L2-resident) is staged per step, through a 3-buffer ring. The step structure
     // is DEPTH 6's: step-1 fragments read under step-0 MFMAs, ONE raw barrier per step, then
     // the freed weight buffer is refilled with step s+3 and step-0 fragments of s+1 are read,
-    // interleaved with step-1 MFMAs. DEPTH 7 double-buffers the halo: chunk c+1's window is
-    // issued one 1-KiB piece per step during chunk c (a wave has at most 8 pieces; the 9th slot
-    // and unused ones DMA the zero page into a junk KiB, so every step issues exactly NL DMAs
-    // and one counted vmcnt covers them). DEPTH 8: a single chunk (C = 64), one halo buffer.
-    // RAW: a weight tile / halo piece issued in iteration i is retired by the vmcnt(NL) of
-    // iteration i+2 (the NL youngest are iteration i+1's), before that iteration's barrier;
-    // chunk c+1's pieces go out in iterations 9c-1 .. 9c+6 and are first read after the
-    // barrier of iteration 9c+8. WAR: the weight buffer of step s is refilled after the
-    // barrier that follows its last reads; halo buffer (c+1)&1 held chunk c-1, last read
-    // before the barrier of iteration 9c-1, refilled from after that barrier on.
+    // interleaved with step-1 MFMAs. The 9 taps of a chunk are unrolled: every tap-dependent
+    // quantity (fragment address variant, weight ring buffer — 9 steps per chunk keep the
+    // ring's phase —, halo piece of the step) is a compile-time constant, and an A fragment
+    // address is ONE VALU op (precomputed lane base + the tap's uniform row offset).
+    // DEPTH 7 double-buffers the halo: chunk c+1's window is issued one 1-KiB piece per step
+    // during chunk c (a wave has at most 8 pieces; the 9th slot and unused ones DMA the zero
+    // page into a junk KiB, so every step issues exactly NL DMAs and one counted vmcnt covers
+    // them). DEPTH 8: a single chunk (C = 64), one halo buffer.
+    // RAW: a weight tile / halo piece issued in step i (after its barrier) is retired by the
+    // vmcnt(NL) of step i+2 (the NL youngest are step i+1's), before that step's barrier;
+    // chunk c+1's pieces go out in steps 9c-1 .. 9c+6 and are first read after the barrier of
+    // step 9c+8. WAR: the weight buffer of step s is refilled after the barrier that follows
+    // its last reads; halo buffer (c+1)&1 held chunk c-1, last read before the barrier of step
+    // 9c-1, refilled from after that barrier on.
     constexpr int NW = NT / 64;
     constexpr int NHB = DEPTH == 7 ? 2 : 1;
     constexpr int HKB = tap_halo_kb(BM);
     constexpr int NHW = (HKB + NW - 1) / NW;    // halo pieces per wave per chunk (max)
     static_assert(DEPTH == 8 || NHW <= 8, "a chunk's halo pieces must be issued within 8 steps");
     constexpr int NL = T::B_CH + (DEPTH == 7 ? 1 : 0);   // LDS-DMAs per wave per step
+    // fragment-address variants per row: the swizzle phase of tap (rr, ss) is
+    // (F0 + ss + t_ky·rr) & 7 with t_ky in {0, 4} (4 only for 4x4 images, BM = 128 tiles):
+    // it depends on ss and, for t_ky = 4, on rr & 1
+    constexpr int NV = BM == 128 ? 6 : 3;
     unsigned char* const junk = smem + NHB * HKB * 1024;
     unsigned char* const bring = junk + 1024;
     const int HW = g.H * g.W;
     const int nimg0 = m0 / HW;
     const int y0 = p.t_imgs > 0 ? 0 : (m0 - nimg0 * HW) / g.W;   // t_imgs 0: a band of one image
     const int nch = p.t_nch;
-    const int nk7 = 9 * nch;
     // halo pieces of this wave: piece wvu + NW·i; lane L carries pixel 8·piece + L/8, physical
     // chunk L%8 = logical chunk (L%8) ^ swizzle. Source element (chunk 0) or -1 (zero: pad ring,
     // images past N, pixels past the window)
-    // (9 slots: the in-loop halo slot of the step with tap j uses slot 0 and then rotates the
-    // slots by one, so slot 0 always holds piece j's source without a dynamic index, which
-    // hipcc would serve from scratch)
-    // (DEPTH 8 issues all its pieces in the prologue only: NHW may exceed 9 there)
-    int hsrc[NHW > 9 ? NHW : 9];
-#pragma unroll
-    for (int i = NHW; i < 9; ++i) hsrc[i] = -1;
+    int hsrc[NHW];
 #pragma unroll
     for (int i = 0; i < NHW; ++i) {
       const int P = (wvu + NW * i) * 8 + (lane >> 3);
@@ -1089,9 +1090,10 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
       const gptr16 s = (real && src >= 0) ? (gptr16)(p.a + src + ch * 64) : zp;
       glds16(s, dst);
     };
-    // A fragment rows: za = (halo row of the lane's output pixel at tap (0, 0))·128 + its
-    // swizzle phase; a tap adds a uniform (row offset·128 + phase offset)
-    int za[TM];
+    // A fragment lane bases: za[i][v] = byte address (step 0 of the k-step pair, u = 0) of the
+    // lane's output pixel's halo row at tap column ss = v % 3 (and rr parity v / 3), swizzle
+    // applied; a tap adds rr·t_rs·128 (+ the halo buffer), k-step u = 1 flips bit 6
+    int za[TM][NV];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = wm * WTM + 16 * i + c;
@@ -1106,29 +1108,36 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         y = ml / g.W;
         x = ml - y * g.W;
       }
-      za[i] = (img * p.t_is + y * p.t_rs + x) * 128 + ((x + p.t_ky * y) & 7);
+      const int P0 = img * p.t_is + y * p.t_rs + x, F0 = x + p.t_ky * y;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int ss = v % 3, rpar = v / 3;
+        za[i][v] = (P0 + ss) * 128 + ((h ^ ((F0 + ss + p.t_ky * rpar) & 7)) << 4);
+      }
     }
-    // uniform part of a step's A address: halo buffer + tap (FWD reads input row y + r − 1 =
-    // halo row y + r; DGRAD reads dy row y + 1 − r = halo row y + 2 − r)
-    auto hoff = [&](int r, int s, int ch) {
-      const int rr = MODE == MODE_FWD ? r : 2 - r, ss = MODE == MODE_FWD ? s : 2 - s;
-      return (NHB == 2 ? (ch & 1) * (HKB * 1024) : 0) + (rr * p.t_rs + ss) * 128 + ss + p.t_ky * rr;
-    };
-    auto read_a7 = [&](int ho, int u, bf16x8 (&af)[TM]) {
+    const int rs128 = p.t_rs * 128;
+    // A fragments of tap TAP (static) of chunk ch, k-step U (static)
+    auto read_a7 = [&](auto TAPc, int ch, auto Uc, bf16x8 (&af)[TM]) {
+      constexpr int tap = decltype(TAPc)::value, u = decltype(Uc)::value;
+      constexpr int rr = MODE == MODE_FWD ? tap / 3 : 2 - tap / 3;
+      constexpr int ss = MODE == MODE_FWD ? tap % 3 : 2 - tap % 3;
+      constexpr int v = NV == 6 ? ss + 3 * (rr & 1) : ss;
+      const int off = (NHB == 2 ? (ch & 1) * (HKB * 1024) : 0) + rr * rs128;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int w = za[i] + ho;
-        const int a = (w & ~127) | ((((w & 7) ^ (4 * u + h))) << 4);
+        const int a = (u ? (za[i][v] ^ 64) : za[i][v]) + off;
         af[i] = *reinterpret_cast<const bf16x8*>(smem + a);
       }
     };
-    auto read_b7 = [&](int bb, int u, bf16x8 (&bfr)[TN]) {
+    auto read_b7 = [&](auto BBc, auto Uc, bf16x8 (&bfr)[TN]) {
+      constexpr int bb = decltype(BBc)::value, u = decltype(Uc)::value;
       const unsigned char* sb = bring + bb * T::B_BYTES;
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = frag_kin(sb, wn * WTN + 16 * j + c, u);
     };
-    // weight tile of step (r, s, ch) into ring buffer bb (past the last step: the zero page)
-    auto issue_b7 = [&](int r, int s, int ch, int bb) {
+    // weight tile of tap TAP of chunk ch into ring buffer TAP % 3 (past the last chunk: zero page)
+    auto issue_b7 = [&](auto TAPc, int ch) {
+      constexpr int tap = decltype(TAPc)::value, r = tap / 3, s = tap % 3, bb = tap % 3;
       const bool kok = ch < nch;
       const int kb = p.b_t0 + r * p.b_tr + s * p.b_ts + ch * 64 + kin_ch * 8;
 #pragma unroll
@@ -1139,83 +1148,62 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
         glds16(src, bring + bb * T::B_BYTES + 8 * (wvu * T::B_CH + i) * BK * 2);
       }
     };
-    // the halo slot of the iteration that reads step (rc, sc, cc): piece 3·rc + sc of chunk cc+1
-    auto halo_slot = [&](int rc, int sc, int cc) {
+    // the halo slot of the step that reads tap J of chunk cc (after its barrier): piece J of
+    // chunk cc + 1 (into halo buffer (cc + 1) & 1), or a junk DMA
+    auto halo_slot = [&](auto Jc, int cc) {
       if constexpr (DEPTH == 7) {
-        const int j = 3 * rc + sc;
-        halo_piece(j, hsrc[0], cc + 1, (cc + 1) & 1, j < NHW && cc + 1 < nch);
-        const int t = hsrc[0];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) hsrc[q] = hsrc[q + 1];
-        hsrc[8] = t;
+        constexpr int j = decltype(Jc)::value;
+        if constexpr (j < NHW) halo_piece(j, hsrc[j], cc + 1, (cc + 1) & 1, cc + 1 < nch);
+        else glds16(zp, junk);
       }
     };
-    auto adv = [](int& r, int& s, int& ch) {
-      s += 1;
-      const bool w1 = s == 3;
-      s = w1 ? 0 : s;
-      r += w1 ? 1 : 0;
-      const bool w2 = r == 3;
-      r = w2 ? 0 : r;
-      ch += w2 ? 1 : 0;
-    };
-    // prologue: chunk 0's window, the weight tiles of steps 0-2 (+ the halo slots of
-    // iterations -3, -2 (none) and -1 (piece 0 of chunk 1))
+    // prologue: chunk 0's window, the weight tiles of taps 0-2 (+ the halo slots of steps
+    // -3, -2 (none) and -1 (piece 0 of chunk 1))
 #pragma unroll
     for (int i = 0; i < NHW; ++i) halo_piece(i, hsrc[i], 0, 0, true);
-    int ir = 0, is = 0, ic = 0;   // weight-issue step
-    issue_b7(ir, is, ic, 0);
-    adv(ir, is, ic);
-    if constexpr (DEPTH == 7) halo_piece(0, 0, 0, 0, false);
-    issue_b7(ir, is, ic, 1);
-    adv(ir, is, ic);
-    if constexpr (DEPTH == 7) halo_piece(0, 0, 0, 0, false);
-    issue_b7(ir, is, ic, 2);
-    adv(ir, is, ic);
-    halo_slot(0, 0, 0);
-    vm_wait<2 * NL>();   // chunk 0's window and step 0's weights landed
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    issue_b7(I0{}, 0);
+    if constexpr (DEPTH == 7) glds16(zp, junk);
+    issue_b7(I1{}, 0);
+    if constexpr (DEPTH == 7) glds16(zp, junk);
+    issue_b7(std::integral_constant<int, 2>{}, 0);
+    halo_slot(I0{}, 0);
+    vm_wait<2 * NL>();   // chunk 0's window and tap 0's weights landed
     lds_barrier();
     stamp(1);
     bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
-    int cr = 0, cs = 0, cc = 0, rb = 0;   // read step, its weight buffer
-    read_a7(hoff(0, 0, 0), 0, a0);
-    read_b7(0, 0, b0);
-    for (int kt = 0; kt < nk7; ++kt) {
-      if (!(SDX_W1_ABL && (p.ablate & 8))) {
-        read_a7(hoff(cr, cs, cc), 1, a1);
-        read_b7(rb, 1, b1);
-      }
-      if (!(SDX_W1_ABL && (p.ablate & 4))) mfma_u(a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt < 160) stamp(2 + 3 * kt);
-      vm_wait<NL>();
-      lds_barrier();
-      if (kt < 160) stamp(3 + 3 * kt);
-      const int fb = rb;
-      adv(cr, cs, cc);
-      rb = rb == 2 ? 0 : rb + 1;
-      // step kt+1 (at kt = nk7-1 a harmless read inside the LDS image, never used)
-      if (!(SDX_W1_ABL && (p.ablate & 8))) {
-        read_a7(hoff(cr, cs, NHB == 2 ? cc : 0), 0, a0);
-        read_b7(rb, 0, b0);
-      }
-      if (!(SDX_W1_ABL && (p.ablate & 2))) {
-        issue_b7(ir, is, ic, fb);
-        halo_slot(cr, cs, cc);
-      } else {
-        // timing ablation: keep the per-step DMA count (the counted vmcnt) with zero-page DMAs
-#pragma unroll
-        for (int i = 0; i < NL; ++i) glds16(zp, junk);
-      }
-      adv(ir, is, ic);
-      if (!(SDX_W1_ABL && (p.ablate & 4))) mfma_u(a1, b1);
-      if constexpr (SDX_W1_SGB) static_for<0, TM * TN>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // up to 5 VALU
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // up to 1 VMEM read (LDS-DMA)
-        __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);   // up to 2 SALU
+    read_a7(I0{}, 0, I0{}, a0);
+    read_b7(I0{}, I0{}, b0);
+    for (int ch = 0; ch < nch; ++ch) {
+      static_for<0, 9>([&](auto TAPc) {
+        constexpr int tap = decltype(TAPc)::value;
+        constexpr int tap1 = (tap + 1) % 9, tap3 = (tap + 3) % 9;
+        const int ch1 = tap == 8 ? ch + 1 : ch;          // chunk of the next step
+        const int ch3 = tap + 3 >= 9 ? ch + 1 : ch;      // chunk of step + 3
+        read_a7(TAPc, ch, I1{}, a1);
+        read_b7(std::integral_constant<int, tap % 3>{}, I1{}, b1);
+        mfma_u(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int kt = 9 * ch + tap;
+        if (kt < 160) stamp(2 + 3 * kt);
+        vm_wait<NL>();
+        lds_barrier();
+        if (kt < 160) stamp(3 + 3 * kt);
+        // the next step (after the last one: a harmless read inside the LDS image, never used)
+        read_a7(std::integral_constant<int, tap1>{}, NHB == 2 ? ch1 : 0, I0{}, a0);
+        read_b7(std::integral_constant<int, tap1 % 3>{}, I0{}, b0);
+        issue_b7(std::integral_constant<int, tap3>{}, ch3);
+        halo_slot(std::integral_constant<int, tap1>{}, ch1);
+        mfma_u(a1, b1);
+        if constexpr (SDX_W1_SGB) static_for<0, TM * TN>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // up to 5 VALU
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // up to 1 VMEM read (LDS-DMA)
+          __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);   // up to 2 SALU
+        });
+        __builtin_amdgcn_sched_barrier(0);
       });
-      __builtin_amdgcn_sched_barrier(0);
     }
     // the zero-page DMAs past the end must land before any wave's epilogue reuses the LDS
     vm_wait<0>();
@@ -2033,6 +2021,7 @@ bool tap_geom(IgemmParams& p, int bm, int depth, int mode) {
   p.t_ky = g.W == 4 ? 4 : 0;
   p.t_nch = cdim / 64;
   if (p.t_nhp > tap_halo_kb(bm)) return false;
+  if (bm == 256 && p.t_ky != 0) return false;   // the BM = 256 loop keeps 3 address variants
   if (depth == 8 && p.t_nch != 1) return false;
   return true;
 }

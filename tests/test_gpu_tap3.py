@@ -135,10 +135,9 @@ def test_tap3_dgrad_bnstat(gpu, shape):
     assert torch.allclose(s_tap, s_ref, rtol=1e-3, atol=1e-1)
 
 
-@pytest.mark.parametrize("shape", [(4, 32, 64, 64), (16, 4, 512, 512)])
+@pytest.mark.parametrize("shape", [(4, 32, 64, 64), (4, 16, 128, 128), (8, 8, 256, 256), (16, 4, 512, 512)])
 def test_tap3_auto_dispatch(gpu, shape):
-    """auto (cfg -1, SDX_TAP3=1 default policy) runs the tap-reuse loop where it measured
-    faster: the layer-1 shape (cfg 11) and 4x4 images (cfg 13)."""
+    """auto (cfg -1) runs the tap-reuse loop on every CIFAR ResNet 3x3 stride-1 shape."""
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
     N, H, C, K = shape
