@@ -157,6 +157,10 @@ void sweep() {
     const hipError_t q = hipEventQuery(c->ev);
     if (q == hipSuccess) {
       continue;
+    } else if (q >= hipErrorStreamCaptureUnsupported && q <= hipErrorStreamCaptureWrongThread) {
+      // a stream capture (hipGraph) in progress on another thread refuses the query: no
+      // verdict this sweep (the deadline keeps running from the armed record)
+      continue;
     } else if (q == hipErrorNotReady) {
       const double waited = 1e-9 * (double)(now_ns() - c->armed_at.load());
       if (waited > c->timeout_s) {

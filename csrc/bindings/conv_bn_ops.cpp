@@ -8,6 +8,7 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <atomic>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -67,12 +68,19 @@ int pinned_cfg() {
 // profiles/tap3_r5.txt) it beats the best implicit-GEMM tile at every CIFAR ResNet-50 3x3:
 // fwd / dgrad l1 52 / 51 vs 67 / 68 us, l2 45 / 42 vs 47 / 45, l3 34 / 34 vs 38 / 37,
 // l4 38 / 38 vs 58 / 56
-int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, bool plain) {
-  static const int tap = [] {
+std::atomic<int>& tap3_flag() {
+  static std::atomic<int> on{[] {
     const char* e = getenv("SDX_TAP3");
     return e == nullptr ? 1 : atoi(e);
-  }();
-  if (tap > 0 && plain && pinned_cfg() < 0) {
+  }()};
+  return on;
+}
+
+// runtime switch of the tap-reuse loop (tests / in-process A/B); returns the previous value
+int64_t tap3_set(int64_t on) { return tap3_flag().exchange((int)on); }
+
+int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, bool plain) {
+  if (tap3_flag().load(std::memory_order_relaxed) > 0 && plain && pinned_cfg() < 0) {
     const int t = igemm_tap_cfg(g, cdim, ncol);
     if (t >= 0) return t;
   }
@@ -118,76 +126,10 @@ int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
 
 namespace {
 
-// In-kernel BN-statistics reduction (StatFuse, launchers.h) requested by a caller of
-// conv_fwd_impl / conv_dgrad_bnstat_impl: the per-channel epilogue (0 sums only — SyncBN
-// all-reduces next, 1 BN finalize, 2 BN-backward coefficients) runs in the conv's last
-// block; `sums` ([nsets][C] fp64) is filled in. Replaces a column-reduce launch per BN.
-struct FuseReq {
-  int epi = 0;
-  BnFinalizeArgs fa{};
-  BnCoefArgs ca{};
-  torch::Tensor sums;
-};
-
-// SDX_STAT_FUSE bits (or stat_fuse_set): 1 forward convs, 2 backward dgrads. Default 0
-// (separate column-reduce launches): measured 13.84 vs 14.02 ms/step with both bits on the
-// same box — the last arriver's serial reduction of ~sqrt(m_tiles) slab rows lands on each
-// conv's critical tail and costs as much as the wide reduction launch it replaces
-// (profiles/ablate_reduce_r2.txt).
-std::atomic<int>& stat_fuse_flag() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("SDX_STAT_FUSE");
-    return e == nullptr ? 0 : atoi(e);
-  }()};
-  return on;
-}
-
-bool stat_fuse_enabled(int bit) { return (stat_fuse_flag().load(std::memory_order_relaxed) & bit) != 0; }
-
-int64_t stat_fuse_set(int64_t bits) { return stat_fuse_flag().exchange((int)bits); }
-
-// ticket counters of the in-kernel reduction: zeroed once per device, reset by the kernels'
-// last arrivers; rotating slots (as reduce_counters) so launches on different streams never
-// share one
-unsigned* fuse_counters(const torch::Device& dev, int n) {
-  constexpr int kSlots = 128, kPerSlot = 8192;
-  TORCH_CHECK(n >= 1 && n <= kPerSlot, "StatFuse: ", n, " counters exceed a slot");
-  static std::mutex mu;
-  static std::map<int, std::pair<torch::Tensor, int>> pool;
-  std::lock_guard<std::mutex> lk(mu);
-  auto& e = pool[dev.index()];
-  if (!e.first.defined())
-    e.first = torch::zeros({kSlots * kPerSlot}, torch::TensorOptions().dtype(at::kInt).device(dev));
-  const int slot = e.second;
-  e.second = (slot + 1) % kSlots;
-  return reinterpret_cast<unsigned*>(e.first.data_ptr<int>()) + slot * kPerSlot;
-}
-
-// StatFuse plan of an M x Ncol GEMM run with tile config cfg; lvl2 keeps the level-2 rows
-// alive until the call returns (stream-ordered reuse by the caching allocator)
-StatFuse make_fuse(FuseReq& r, const torch::Tensor& like, int64_t M, int64_t Ncol, int cfg, int nsets,
-                   torch::Tensor& lvl2) {
-  const int mt = (int)((M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg));
-  const int nt = (int)((Ncol + igemm_tile_n(cfg) - 1) / igemm_tile_n(cfg));
-  StatFuse f{};
-  f.group = stat_fuse_groups(mt);
-  f.n_groups = (mt + f.group - 1) / f.group;
-  f.cnt = fuse_counters(like.device(), stat_fuse_counters(mt, nt));
-  auto dopt = like.options().dtype(at::kDouble);
-  lvl2 = torch::empty({(int64_t)f.n_groups * nsets * Ncol}, dopt);
-  r.sums = torch::empty({nsets, Ncol}, dopt);
-  f.lvl2 = lvl2.data_ptr<double>();
-  f.sums = r.sums.data_ptr<double>();
-  f.epi = r.epi;
-  f.fa = r.fa;
-  f.ca = r.ca;
-  return f;
-}
-
 // no_out: statistics only, the output is not stored (first pass of a forward-folded BN3)
 std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad,
                                          bool want_stats, int64_t cfg, OptT in_scale, OptT in_shift,
-                                         FuseReq* fr, const GemmEpi* epi = nullptr, bool no_out = false) {
+                                         const GemmEpi* epi = nullptr, bool no_out = false) {
   check_bf16_nhwc(x, "x");
   check_bf16_nhwc(w, "w");
   TORCH_CHECK(w.size(3) == x.size(3), "weight Cin != input C");
@@ -203,8 +145,8 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
   c10::DeviceGuard dg(x.device());
   const int64_t M = (int64_t)g.N * g.P * g.Q;
   if (cfg < 0)
-    cfg = conv_cfg(g, g.C, g.K, M, (int64_t)g.R * g.S * g.C, fr == nullptr && !in_scale.has_value());
-  TORCH_CHECK(!no_out || (want_stats && fr == nullptr && epi == nullptr), "statistics-only conv: stats, no epilogue");
+    cfg = conv_cfg(g, g.C, g.K, M, (int64_t)g.R * g.S * g.C, !in_scale.has_value());
+  TORCH_CHECK(!no_out || (want_stats && epi == nullptr), "statistics-only conv: stats, no epilogue");
   auto y = no_out ? torch::Tensor() : torch::empty({g.N, g.P, g.Q, g.K}, x.options());
   torch::Tensor slab;
   float* sp = nullptr;
@@ -217,14 +159,8 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
   }
   const float *isc, *ish;
   in_bn_ptrs(in_scale, in_shift, g.C, &isc, &ish);
-  StatFuse sf{};
-  torch::Tensor lvl2;
-  if (fr != nullptr) {
-    TORCH_CHECK(want_stats && isc == nullptr, "StatFuse: statistics without the BN prologue only");
-    sf = make_fuse(*fr, x, M, g.K, (int)cfg, 2, lvl2);
-  }
   check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), no_out ? nullptr : y.data_ptr(), sp, (int)cfg, cur_stream(),
-                            isc, ish, epi, fr != nullptr ? &sf : nullptr),
+                            isc, ish, epi),
             "conv_fwd");
   return {y, slab};
 }
@@ -238,12 +174,12 @@ torch::Tensor conv_fwd_bias(torch::Tensor x, torch::Tensor w, int64_t stride, in
   GemmEpi epi{};
   epi.bias = bias.data_ptr<float>();
   epi.relu = relu ? 1 : 0;
-  return conv_fwd_impl(x, w, stride, pad, false, -1, c10::nullopt, c10::nullopt, nullptr, &epi)[0];
+  return conv_fwd_impl(x, w, stride, pad, false, -1, c10::nullopt, c10::nullopt, &epi)[0];
 }
 
 std::vector<torch::Tensor> conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, bool want_stats,
                                     int64_t cfg, OptT in_scale, OptT in_shift) {
-  return conv_fwd_impl(x, w, stride, pad, want_stats, cfg, in_scale, in_shift, nullptr);
+  return conv_fwd_impl(x, w, stride, pad, want_stats, cfg, in_scale, in_shift);
 }
 
 // bs (optional): fused BN-backward statistics; its slab must hold conv_dgrad_slab_rows rows
@@ -265,8 +201,7 @@ struct AddPreScope {
 
 torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                               int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
-                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0,
-                              FuseReq* fr = nullptr) {
+                              c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
   TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
@@ -279,7 +214,7 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
   c10::DeviceGuard dg(dy.device());
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), fr == nullptr);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true);
   torch::Tensor dx;
   if (out.has_value()) {
     dx = *out;
@@ -313,17 +248,12 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     amask = addend_mask->data_ptr();
   }
   if (bs) bs->row0 = 0;
-  TORCH_CHECK(fr == nullptr || (bs != nullptr && stride == 1), "StatFuse: single-launch statistics dgrads only");
   if (stride == 1) {
-    StatFuse sf{};
-    torch::Tensor lvl2;
-    if (fr != nullptr) sf = make_fuse(*fr, dy, M, g.C, (int)cfg, bs->yb != nullptr ? 3 : 2, lvl2);
     // BN3 fold: the addend joins the accumulators before rounding (kernels built with SDX_ADD_PRE)
     static const GemmEpi pre{nullptr, 0, 0, 1};
     const GemmEpi* epi = (fold_add_pre() && add != nullptr && addend_sub == 0 && amask == nullptr) ? &pre : nullptr;
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
-                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0, epi,
-                                      fr != nullptr ? &sf : nullptr),
+                                      cur_stream(), amask, bs, add ? (int)addend_sub : 0, epi),
               "conv_dgrad");
     return dx;
   }
@@ -367,7 +297,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
                                                   int64_t stride, int64_t pad, int64_t cfg, OptT out, OptT addend,
                                                   OptT addend_mask, torch::Tensor ya, torch::Tensor ma, OptT yb,
                                                   OptT mb, OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub,
-                                                  FuseReq* fr, int store_masked = 0, int64_t extra_rows = 0) {
+                                                  int store_masked = 0, int64_t extra_rows = 0) {
   const int64_t C = wt.size(0);
   // an empty ya: the BN input was never stored (forward-folded BN3) — the epilogue sums
   // Σdz and Σdz·(0 − μ); the caller fills extra_rows rows of the slab with the Σdz·y terms
@@ -408,7 +338,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   g.C = C; g.R = wt.size(1); g.S = wt.size(2);
   g.H = H; g.W = W; g.stride = stride; g.pad = pad;
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), fr == nullptr);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true);
   int rows = 0;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) rows += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
@@ -417,7 +347,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   bs.slab = slab.data_ptr<float>();
   TORCH_CHECK(!store_masked || (mask_bits.has_value() && stride == 1), "store_masked: stride-1 with a ReLU bitmask");
   bs.store_masked = store_masked;
-  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs, addend_sub, fr);
+  auto dx = conv_dgrad_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, &bs, addend_sub);
   return {dx, slab};
 }
 
@@ -427,7 +357,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat(torch::Tensor dy, torch::Tensor wt,
                                              OptT mask_bits, OptT msc, OptT msh, int64_t addend_sub = 0,
                                              int store_masked = 0, int64_t extra_rows = 0) {
   return conv_dgrad_bnstat_impl(dy, wt, H, W, stride, pad, cfg, out, addend, addend_mask, ya, ma, yb, mb, mask_bits,
-                                msc, msh, addend_sub, nullptr, store_masked, extra_rows);
+                                msc, msh, addend_sub, store_masked, extra_rows);
 }
 
 }  // namespace
@@ -1030,32 +960,14 @@ BnState bn_forward(const torch::Tensor& slab, double count, const torch::Tensor&
 
 double rows_of(const torch::Tensor& y) { return (double)(y.numel() / y.size(3)); }
 
-// conv + BN forward statistics. Training with StatFuse: the conv's last block reduces the
-// statistics and (one rank) finalizes the BN in the same launch; SyncBN: it leaves the sums
-// for the in-place all-reduce, then one finalize launch.
+// conv + BN forward: the conv's epilogue emits per-tile statistics, one launch reduces and
+// finalizes them (or reduce -> SyncBN exchange -> finalize)
 std::pair<torch::Tensor, BnState> conv_bn_fwd(const torch::Tensor& x, const torch::Tensor& w, int64_t stride,
                                               int64_t pad, const torch::Tensor& g, const torch::Tensor& b,
                                               const torch::Tensor& rm, const torch::Tensor& rv, double eps,
                                               double mom, bool training, int64_t comm) {
-  if (!training || !stat_fuse_enabled(1)) {
-    auto c = conv_fwd(x, w, stride, pad, training, -1, c10::nullopt, c10::nullopt);
-    return {c[0], bn_forward(c[1], rows_of(c[0]), g, b, rm, rv, eps, mom, training, comm)};
-  }
-  const bool sync = comm != 0 && small_comm_world(comm) > 1;
-  FuseReq fr;
-  FinalizeOut o;
-  const int64_t C = w.size(0);
-  if (!sync) {
-    // count: output rows; known before the launch from the geometry
-    const int64_t P = (x.size(1) + 2 * pad - w.size(1)) / stride + 1, Q = (x.size(2) + 2 * pad - w.size(2)) / stride + 1;
-    fr.epi = 1;
-    fr.fa = finalize_args(x, C, (double)(x.size(0) * P * Q), g, b, eps, mom, true, rm, rv, o);
-  }
-  auto c = conv_fwd_impl(x, w, stride, pad, true, -1, c10::nullopt, c10::nullopt, &fr);
-  if (!sync) return {c[0], BnState{o.scale, o.shift, o.mean, o.invstd}};
-  small_all_reduce_(comm, fr.sums);
-  auto r = bn_finalize(fr.sums, rows_of(c[0]) * small_comm_world(comm), g, b, eps, mom, true, rm, rv);
-  return {c[0], BnState{r[0], r[1], r[2], r[3]}};
+  auto c = conv_fwd(x, w, stride, pad, training, -1, c10::nullopt, c10::nullopt);
+  return {c[0], bn_forward(c[1], rows_of(c[0]), g, b, rm, rv, eps, mom, training, comm)};
 }
 
 // bn_bwd_reduce_coef, or (communicator of >1 ranks) reduce -> in-place all-reduce of the
@@ -1336,7 +1248,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   // read there after the join), the side stream only writes them
   torch::Tensor ys_side, slab_side;
   hipEvent_t sc_done = nullptr;
-  if (proj && training && side != 0 && !stat_fuse_enabled(1)) {
+  if (proj && training && side != 0) {
     const torch::Tensor& ws = w[nconv];
     check_bf16_nhwc(x, "x");
     check_bf16_nhwc(ws, "w_shortcut");
@@ -1380,7 +1292,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
     if (fold_fwd) {
       // pass 1: BN3 statistics (nothing stored) -> finalize (SyncBN: fused exchange) ;
       // pass 2: out = relu(bn3(y3) + x) and its bits straight from conv3's epilogue
-      auto c3s = conv_fwd_impl(a2, w[2], 1, 0, true, -1, c10::nullopt, c10::nullopt, nullptr, nullptr, true);
+      auto c3s = conv_fwd_impl(a2, w[2], 1, 0, true, -1, c10::nullopt, c10::nullopt, nullptr, true);
       st.push_back(bn_forward(c3s[1], rows_of(a2), B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm));
       omask = torch::empty({x.numel() / 8}, x.options().dtype(at::kByte));
       GemmEpi epi{};
@@ -1388,7 +1300,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
       epi.bn_shift = st[2].sh.data_ptr<float>();
       epi.resid = x.data_ptr();
       epi.mask_out = omask.data_ptr<uint8_t>();
-      o = conv_fwd_impl(a2, w[2], 1, 0, false, -1, c10::nullopt, c10::nullopt, nullptr, &epi)[0];
+      o = conv_fwd_impl(a2, w[2], 1, 0, false, -1, c10::nullopt, c10::nullopt, &epi)[0];
       last = torch::Tensor();
     } else {
       auto c3 = conv_bn_fwd(a2, w[2], 1, 0, B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm);
@@ -1551,26 +1463,6 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   // Σda·m, Σda·m·(y−μ) come from the dgrad epilogue (SDX_DGRAD_BNSTAT=0: separate pass)
   auto dgrad_bn = [&](const torch::Tensor& dyo, const torch::Tensor& w, const torch::Tensor& y, int64_t st,
                       int64_t pad, int i, double cnt, OptT add = c10::nullopt) -> std::pair<torch::Tensor, torch::Tensor> {
-    if (dgrad_bnstat_enabled() && st == 1 && stat_fuse_enabled(2)) {
-      // the dgrad's last block reduces the statistics and (one rank) evaluates the coefficients
-      const bool sync = comm != 0 && small_comm_world(comm) > 1;
-      FuseReq fr;
-      CoefOut o;
-      if (!sync) {
-        fr.epi = 2;
-        fr.ca = coef_args(y, y.size(3), 1, cnt, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt, c10::nullopt,
-                          G(i, 1), G(i, 2), c10::nullopt, c10::nullopt, o);
-      }
-      auto r = conv_dgrad_bnstat_impl(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, add,
-                                      c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0),
-                                      S(i, 1), 0, &fr);
-      if (!sync) return {r[0], o.coef_a};
-      small_all_reduce_(comm, fr.sums);
-      const int wsz = small_comm_world(comm);
-      auto c = bn_bwd_coef(fr.sums, cnt * wsz, G(i, 0), S(i, 2), S(i, 3), c10::nullopt, c10::nullopt, c10::nullopt,
-                           G(i, 1), G(i, 2), c10::nullopt, c10::nullopt, 1.0 / wsz);
-      return {r[0], c[0]};
-    }
     if (dgrad_bnstat_enabled()) {
       auto r = conv_dgrad_bnstat(dyo, w, y.size(1), y.size(2), st, pad, -1, c10::nullopt, add,
                                  c10::nullopt, y, S(i, 2), c10::nullopt, c10::nullopt, c10::nullopt, S(i, 0), S(i, 1));
@@ -1698,12 +1590,11 @@ void register_conv_bn(pybind11::module& m) {
         "implicit-GEMM conv forward with a per-channel fp32 bias (+ReLU) epilogue (eval-mode folded BN)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("bias"),
         pybind11::arg("relu"));
+  m.def("tap3_set", &tap3_set,
+        "tap-reuse 3x3 conv loop on (1) / off (0) for auto tile selection; returns the previous value",
+        pybind11::arg("on"));
   m.def("syncbn_exchange_sums", &syncbn_exchange_sums,
         "column reduction + cross-rank exchange of a BN statistics slab in one launch (fused xGMI communicators)");
-  m.def("stat_fuse_set", &stat_fuse_set,
-        "in-kernel BN-statistics reduction of the block executor (bits: 1 forward, 2 backward); returns the "
-        "previous bits",
-        pybind11::arg("bits"));
   m.def("igemm_trace", [] {
     const int n = 2 * igemm_trace_slots();
     auto t = torch::empty({n}, torch::TensorOptions().dtype(at::kLong));

@@ -77,8 +77,25 @@ void wprep(torch::Tensor master, torch::Tensor out, torch::Tensor segs, int64_t 
             "wprep");
 }
 
+// dst (fp32 [..., C], contiguous) += src[..., :C] (fp32 [..., Cp], contiguous), same leading dims
+void unpad_add(torch::Tensor src, torch::Tensor dst) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kFloat && src.is_contiguous(), "src fp32 contiguous");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst fp32 contiguous");
+  TORCH_CHECK(src.dim() == dst.dim() && src.dim() >= 1, "same rank");
+  for (int64_t d = 0; d + 1 < src.dim(); ++d) TORCH_CHECK(src.size(d) == dst.size(d), "leading dims");
+  const int64_t Cp = src.size(-1), C = dst.size(-1);
+  TORCH_CHECK(C <= Cp && src.numel() / Cp * C < (1LL << 31), "C <= Cp");
+  c10::DeviceGuard dg(src.device());
+  check_hip(launch_unpad_add(src.data_ptr<float>(), dst.data_ptr<float>(), (int)(src.numel() / Cp), (int)Cp, (int)C,
+                             cur_stream()),
+            "unpad_add");
+}
+
 }  // namespace
 
-void register_wprep(pybind11::module& m) { m.def("wprep", &wprep, "fp32 master -> bf16 fwd/dgrad conv weights"); }
+void register_wprep(pybind11::module& m) {
+  m.def("wprep", &wprep, "fp32 master -> bf16 fwd/dgrad conv weights");
+  m.def("unpad_add", &unpad_add, "dst += src[..., :C] of a channel-padded fp32 tensor");
+}
 
 }  // namespace sdx_bind

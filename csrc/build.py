@@ -88,14 +88,23 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
               f"-DTORCH_EXTENSION_NAME={name}", f"-I{py_inc}"] + [f"-I{p}" for p in inc_torch] + common + \
         (SAN_FLAGS if sanitize else [])
-    hdr_m = _headers_mtime()
     kern, bind = _sources()
 
+    # objects are keyed on the flags and the CONTENT of the source and of every header (an
+    # mtime test misses an edit made while that source was compiling)
+    hdr_h = hashlib.sha1()
+    hdir = os.path.join(CSRC, "include")
+    for f in sorted(os.listdir(hdir)):
+        with open(os.path.join(hdir, f), "rb") as fh:
+            hdr_h.update(f.encode() + fh.read())
+    hdr_digest = hdr_h.hexdigest()
+
     def job(src, flags):
-        key = hashlib.sha1((" ".join(flags) + src).encode()).hexdigest()[:10]
+        with open(src, "rb") as fh:
+            src_digest = hashlib.sha1(fh.read()).hexdigest()
+        key = hashlib.sha1((" ".join(flags) + src + src_digest + hdr_digest).encode()).hexdigest()[:12]
         obj = os.path.join(OBJ_DIR, os.path.basename(src) + f".{key}.o")
-        if (not force and os.path.exists(obj)
-                and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_m)):
+        if not force and os.path.exists(obj):
             return obj, False
         cmd = flags + ["-c", src, "-o", obj]
         if verbose:

@@ -1,6 +1,5 @@
-// Per-channel BatchNorm epilogues shared by the stand-alone BN kernels (bn.hip), the
-// single-launch column reduction and the in-kernel statistics reduction of the conv GEMMs
-// (igemm.hip StatFuse): forward finalize (affine + running statistics) and backward
+// Per-channel BatchNorm epilogues shared by the stand-alone BN kernels and the single-launch
+// column reduction (bn.hip): forward finalize (affine + running statistics) and backward
 // coefficients (+ dγ/dβ into the gradient sinks).
 #pragma once
 #include "launchers.h"

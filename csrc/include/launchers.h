@@ -101,11 +101,9 @@ int igemm_tile_n(int cfg);
 // cdim channels and whose output has ncol channels (DGRAD: cdim = K, ncol = C), or -1
 int igemm_tap_cfg(const ConvGeom& g, int cdim, int ncol);
 // in_scale/in_shift (optional, [C] fp32): fused BN+ReLU prologue on the input activation
-struct StatFuse;
-// sf (optional, with stats): reduce the statistics slab in-kernel (StatFuse)
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
                            hipStream_t s, const float* in_scale = nullptr, const float* in_shift = nullptr,
-                           const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);
+                           const GemmEpi* epi = nullptr);
 // strided dgrad = stride² sub-pixel classes; wt = the full Wt [C][R][S][K] (each class reads
 // its taps r0::st, s0::st in place)
 void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* s0, int* ns, int* Hc, int* Wc);
@@ -113,15 +111,12 @@ void conv_dgrad_class(const ConvGeom& g, int ph, int pw, int* r0, int* nr, int* 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                    const BnBwdStat* bstat = nullptr, int addend_sub = 0,
-                                   const GemmEpi* epi = nullptr, const StatFuse* sf = nullptr);
+                                   const GemmEpi* epi = nullptr);
 // every sub-pixel class of a strided dgrad (stride 2) in ONE launch; bstat->row0 = the first
 // class's slab row (the classes' rows follow in the kernel's class order)
 hipError_t launch_conv_dgrad_merged(const ConvGeom& g, const void* dy, const void* wt, void* dx, const void* addend,
                                     int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                     const BnBwdStat* bstat = nullptr, int addend_sub = 0);
-// in-kernel statistics reduction plan for an M x Ncol GEMM of tile config cfg
-int stat_fuse_groups(int m_tiles);
-int stat_fuse_counters(int m_tiles, int n_tiles);
 // M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
 int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
@@ -178,24 +173,6 @@ struct BnCoefArgs {
   // bucket reducer's sum × 1/W yields global / W and not the global value.
   double grad_scale = 1.0;
 };
-// In-kernel reduction of a conv GEMM's per-M-tile BN statistics (igemm.hip), replacing the
-// separate column-reduce launch: every block stores its slab row write-through, drains and
-// takes a ticket on its (M-tile group, N-tile) counter; a group's last arriver sums the
-// group's rows (fp64, row order) into a level-2 row and tickets its N-tile counter; the last
-// of those sums the level-2 rows (group order) into `sums` and runs the per-channel epilogue
-// for its columns. Deterministic for any dispatch order or XCD placement.
-struct StatFuse {
-  unsigned* cnt;     // [n_groups * n_tiles] level-1 then [n_tiles] level-2 tickets; zero on
-                     // entry, reset by their last arriver (nullptr: no fusion, slab only)
-  double* lvl2;      // [n_groups][nsets][Ncol]
-  double* sums;      // [nsets][Ncol]
-  int group;         // M-tiles per level-1 group
-  int n_groups;
-  int epi;           // 0 sums only (SyncBN: all-reduce next), 1 BN finalize, 2 BN-bwd coefficients
-  BnFinalizeArgs fa;
-  BnCoefArgs ca;
-};
-
 // ---- xGMI peer arenas (xgmi.hip, bn.hip) ----------------------------------------------
 constexpr int kXgmiMaxPeers = 8;
 constexpr int kXgmiFlagGroups = 64;   // per-sender flags per parity: one per 64-channel column group
@@ -289,6 +266,8 @@ hipError_t launch_gap_bwd(const float* dy, void* dx, int N, int HW, int C, hipSt
 // ---- weight preparation (wprep.hip) ---------------------------------------------
 // segs: device table of nseg rows {src, dst_k, dst_t, K|RS<<32, C|Cp<<32, n, start} (int64)
 hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s);
+// dst[r][c] += src[r][c], c < C, of a channel-padded [rows][Cp] fp32 tensor (stem weight gradient)
+hipError_t launch_unpad_add(const float* src, float* dst, int rows, int Cp, int C, hipStream_t s);
 
 // ---- one-shot small all-reduce over xGMI peer memory (xgmi.hip) --------------------
 // err: host-pinned int (1 + rank of a peer whose flag missed the deadline of timeout_ticks

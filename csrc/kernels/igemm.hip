@@ -29,7 +29,6 @@
 // by igemm_splitk_reduce), never atomics. Block→tile order is XCD-aware.
 #include "common.h"
 #include "launchers.h"
-#include "bn_epilogue.h"
 
 using namespace sdx;
 
@@ -37,14 +36,8 @@ namespace {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int BK = 64;
-#ifndef SDX_FAST_TAPS
-#define SDX_FAST_TAPS 0
-#endif
 #ifndef SDX_PRIO_HALF
 #define SDX_PRIO_HALF 1
-#endif
-#ifndef SDX_FRAG_PIN
-#define SDX_FRAG_PIN 0
 #endif
 #ifndef SDX_W1_ABL
 #define SDX_W1_ABL 0   // DEPTH 6: honour the SDX_IGEMM_ABLATE bits (diagnostic builds only)
@@ -100,7 +93,7 @@ struct IgemmParams {
   const float* in_shift;
   // diagnostic ablation (SDX_IGEMM_ABLATE bits, timing only — results are wrong):
   // 1 skip LDS stores, 2 skip global loads / LDS-DMA, 4 skip MFMAs, 8 skip the fragment
-  // reads (ping-pong loop)
+  // reads (DEPTH 6, builds with SDX_W1_ABL=1)
   int ablate;
   // log2(Q), log2(P*Q) when both are powers of two, else -1 (WGRAD pixel decode)
   int lq, lpq;
@@ -124,8 +117,6 @@ struct IgemmParams {
   uint8_t* mask_out;
   // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
   int worder;
-  // FWD statistics / DGRAD BN-backward statistics reduced in-kernel (sf.cnt != nullptr)
-  StatFuse sf;
   int M, Ncol, Kdim;
   // FWD / DGRAD weight operand addressing: output column col, logical k = (kr, ks, kc) reads
   // b[col·b_row + b_t0 + kr·b_tr + ks·b_ts + kc]. FWD W [K][R][S][Cp] and stride-1 DGRAD Wt
@@ -267,147 +258,20 @@ struct Tile {
   static constexpr int B_CH = BN * BK / 8 / NT;
 };
 
-// write-through (sc1) fp32 / fp64 stores and loads of the statistics hand-off
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// StatFuse tail (launchers.h): run by every thread of a block right after its slab row
-// (row `mt` of [m_tiles][NS][Ncol], stored sc1) is written. Hand-off protocol as in bn.hip
-// col_reduce: every storing wave drains its sc1 stores, a barrier, ONE lane's agent-scope
-// ticket; only the last arriver reads the handed-off rows, all with sc1 loads. Inlined: it
-// runs after the accumulators are dead (a call would impose the ABI: scratch + spills).
-template <int NT, int BN, int NS>
-__device__ __forceinline__ void stat_fuse_tail(const StatFuse& f, const float* slab, int Ncol, int mt, int m_tiles,
-                                            int nt, int n_tiles, int n0, unsigned char* smem) {
-  constexpr int P = NT / BN;                 // row parts per column (NT >= BN for every tile)
-  static_assert(P >= 1 && P * BN == NT, "thread (column, part) layout");
-  const int tid = threadIdx.x, col = tid % BN, part = tid / BN;
-  int* flag = reinterpret_cast<int*>(smem);
-  double* red = reinterpret_cast<double*>(smem + 16);   // [P][NS][BN]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int g = mt / f.group;
-  const int r0 = g * f.group, r1 = min(m_tiles, r0 + f.group);
-  unsigned* c1 = f.cnt + g * n_tiles + nt;
-  unsigned* c2 = f.cnt + f.n_groups * n_tiles + nt;
-  if (tid == 0) {
-    const unsigned t = __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = t == (unsigned)(r1 - r0 - 1);
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  const bool cok = n0 + col < Ncol;
-  // level 1: part p sums the group's rows r0+p, r0+p+P, ... (4 rows in flight), fp64
-  {
-    double acc[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) acc[k] = 0.0;
-    if (cok) {
-      const size_t rs = (size_t)NS * Ncol;              // slab row stride (floats)
-      const float* q = slab + (size_t)(r0 + part) * rs + n0 + col;
-      int r = r0 + part;
-      for (; r + 3 * P < r1; r += 4 * P, q += 4 * P * rs) {
-        float v[4][NS];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int k = 0; k < NS; ++k) v[u][k] = ld_sc1(q + u * P * rs + (size_t)k * Ncol);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int k = 0; k < NS; ++k) acc[k] += (double)v[u][k];
-      }
-      for (; r < r1; r += P, q += P * rs)
-#pragma unroll
-        for (int k = 0; k < NS; ++k) acc[k] += (double)ld_sc1(q + (size_t)k * Ncol);
-    }
-#pragma unroll
-    for (int k = 0; k < NS; ++k) red[(part * NS + k) * BN + col] = acc[k];
-    __syncthreads();
-    if (part == 0 && cok) {
-#pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        double t = 0.0;
-        for (int q = 0; q < P; ++q) t += red[(q * NS + k) * BN + col];
-        st_sc1(f.lvl2 + ((size_t)g * NS + k) * Ncol + n0 + col, t);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(c1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
-    const unsigned t = __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[1] = t == (unsigned)(f.n_groups - 1);
-  }
-  __syncthreads();
-  if (!flag[1]) return;
-  // level 2: part p sums groups p, p+P, ... in order, then the parts in order
-  {
-    double acc[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) acc[k] = 0.0;
-    if (cok)
-      for (int q = part; q < f.n_groups; q += P)
-#pragma unroll
-        for (int k = 0; k < NS; ++k) acc[k] += ld_sc1(f.lvl2 + ((size_t)q * NS + k) * Ncol + n0 + col);
-#pragma unroll
-    for (int k = 0; k < NS; ++k) red[(part * NS + k) * BN + col] = acc[k];
-    __syncthreads();
-    if (part == 0 && cok) {
-      double t[NS];
-#pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        t[k] = 0.0;
-        for (int q = 0; q < P; ++q) t[k] += red[(q * NS + k) * BN + col];
-        f.sums[(size_t)k * Ncol + n0 + col] = t[k];
-      }
-      if constexpr (NS == 2) {
-        if (f.epi == 1) bn_finalize_one(n0 + col, t[0], t[1], f.fa);
-      }
-      if (f.epi == 2) bn_coef_one(n0 + col, Ncol, t, NS - 1, f.ca);
-    }
-  }
-  if (tid == 0) __hip_atomic_store(c2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // DEPTH: 1 / 2 = register-staged operands, 1 or 2 K-tiles of prefetch; 3 = LDS-DMA
 // (global_load_lds) staging of both K-inner operands (FWD / DGRAD without the BN prologue):
 // no staging registers and no ds_write — the ds_write_b128 transfer path was the busiest
 // LDS resource of the register-staged loop.
 // VAR, DGRAD: 1 = fused BN-backward statistics epilogue (p.bs) — a separate variant so
-// the plain dgrad keeps its register budget; 3 = the same plus the in-kernel statistics
-// reduction (p.sf, StatFuse). VAR, FWD: 1 = in-kernel reduction of the BN statistics slab
-// (p.sf). ONE (LDS-DMA, reduction <= BK): a single
+// the plain dgrad keeps its register budget; 2 = the same, storing the gradient ReLU-masked.
+// VAR, FWD: 2 = block-output BN-apply epilogue. ONE (LDS-DMA, reduction <= BK): a single
 // K-tile needs no second LDS buffer; the smaller static LDS (one stage or the C tile) lets
 // twice as many blocks share a CU, hiding the load -> MFMA -> store latency of these
 // memory-bound 1x1 layer-1 GEMMs across blocks.
-// waves/SIMD the register allocator must fit: the StatFuse dgrad variants are held to the
-// occupancy of their plain statistics variant (the tail would otherwise cost one wave)
-template <int MODE, int BM, int BN, int WM, int WN, int VAR>
-constexpr int igemm_min_waves() {
-  // 4-wave blocks of 64x128 / 128x64 wave tiles (DEPTH 6): one wave per SIMD, all registers
-  if (WM * WN == 4 && BM * BN >= 128 * 256) return 1;
-  if (MODE != MODE_DGRAD || VAR != 3) return 2;
-  if (BM == 64 && BN == 64) return 5;
-  return (BM == 128 && BN == 128 && WM * WN == 8) ? 4 : 2;   // the others are at 2 (or 1) anyway
-}
-
+// Every configuration is held to 2 waves per SIMD (<= 256 VGPRs): 8-wave blocks one per CU,
+// 4-wave blocks two per CU.
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR, bool ONE>
-__global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN, VAR>())) void igemm_kernel(
+__global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     IgemmParams p_in) {
   // a block-local copy: a merged strided-dgrad launch overwrites its class's fields (uniform
   // values: SROA keeps the untouched fields in the kernel arguments)
@@ -423,7 +287,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   // slots), a 3-buffer ring of weight tiles
   constexpr int LDS_TAP = (DEPTH == 7 ? 2 : 1) * tap_halo_kb(BM) * 1024 + 1024 + 3 * T::B_BYTES;
   constexpr int LDS = ONE ? (T::STAGE > LDS_C ? T::STAGE : LDS_C)
-                          : DEPTH >= 7 ? LDS_TAP : (DEPTH >= 4 ? 3 : 2) * T::STAGE;
+                          : DEPTH >= 7 ? LDS_TAP : (DEPTH == 6 ? 3 : 2) * T::STAGE;
   static_assert(!ONE || DEPTH == 3, "single-stage variant is LDS-DMA only");
   static_assert(DEPTH < 4 || MODE != MODE_WGRAD, "LDS-DMA ring is FWD/DGRAD only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
@@ -513,7 +377,6 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   // registers otherwise sit in every wgrad main loop (VALU-bound: ~6-10 VALU per MFMA).
   constexpr bool W1X1 = MODE == MODE_WGRAD && (VAR & 1);
   constexpr bool WPRO = MODE == MODE_WGRAD && (VAR & 2);
-  constexpr bool SF = (MODE == MODE_FWD && VAR == 1) || (MODE == MODE_DGRAD && VAR == 3);
   const bool is1x1 = (MODE == MODE_WGRAD) ? W1X1 : (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0);
   // A rows: element offset of the row base, and its spatial origin (FWD: top-left input
   // tap; DGRAD: dy coordinate of tap (r0, s0))
@@ -572,8 +435,7 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
   const int taps = (MODE == MODE_FWD) ? g.R * g.S : p.nr * p.ns;
   // (always on in DEPTH 6, whose host routing guarantees cdim % BK == 0 and taps <= 32: it
   // halves the address VALU of the DMA issue, which is interleaved with the MFMAs there)
-  const bool fast_taps = (DEPTH == 6 && MODE != MODE_WGRAD) ||
-                         (SDX_FAST_TAPS && GL && MODE != MODE_WGRAD && (cdim % BK) == 0 && taps <= 32);
+  const bool fast_taps = DEPTH == 6 && MODE != MODE_WGRAD;
   constexpr int FCH = (GL && MODE != MODE_WGRAD) ? T::A_CH : 1;
   unsigned vmask[FCH];
   int rbase[FCH];
@@ -965,7 +827,6 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     return f;
   };
 
-  constexpr bool FRAG_PIN = SDX_FRAG_PIN;
   // all fragments of both 32-deep k-steps of a K-tile (distinct registers, so the MFMAs of
   // step 0 overlap the LDS latency of step 1 and no lgkmcnt(0) drain sits between MFMA
   // groups: the compiler otherwise recycles two A-fragment registers and stalls on each refill)
@@ -1016,14 +877,12 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     if (p.ablate & 4) return;
     bf16x8 af[2][TM], bfr[2][TN];
     read_frags(buf, af, bfr);
-    if (FRAG_PIN) __builtin_amdgcn_sched_barrier(0);   // keep all fragment reads ahead of the MFMAs
     mfma_tile(af, bfr);
   };
 
   // 8-wave blocks: the second-dispatched half loses VALU/issue arbitration to the older half
   // on every segment; one static priority raise for it (no per-cluster flips). SDX_PRIO_HALF
-  // (not in the ping-pong loop, whose halves take turns by construction)
-  if (SDX_PRIO_HALF && NT == 512 && DEPTH != 5 && __builtin_amdgcn_readfirstlane(tid) >= 256)
+  if (SDX_PRIO_HALF && NT == 512 && __builtin_amdgcn_readfirstlane(tid) >= 256)
     __builtin_amdgcn_s_setprio(1);
   // K loop: two LDS buffers, one barrier per K-tile. DEPTH 1: the loads of tile k+1 are in
   // flight during the MFMAs of tile k. DEPTH 2: two register stages, so tile k+2's loads
@@ -1209,9 +1068,8 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     vm_wait<0>();
     __syncthreads();
   } else if constexpr (DEPTH == 6) {
-    // One wave per SIMD (4-wave block, 64x128 / 128x64 wave tiles: half the LDS fragment
-    // bytes per MFMA of the 8-wave 64x32 tiles) over a 3-buffer LDS-DMA ring, pipelined
-    // inside each wave. A K-tile is two 32-deep k-steps: the fragments of step 1 are read
+    // 8-wave 256x128 / 128x256 tiles (64x64 wave tiles, two waves per SIMD) over a 3-buffer
+    // LDS-DMA ring, pipelined inside each wave. A K-tile is two 32-deep k-steps: the fragments of step 1 are read
     // while step 0's MFMAs run, then ONE raw barrier (every wave's reads of this tile are
     // done and its own DMAs of tile k+1 retired by the counted vmcnt), then the buffer just
     // freed is refilled with tile k+3 and step 0 of tile k+1 is read, both interleaved with
@@ -1260,86 +1118,11 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     // LDS (C staging): this wave's drain, then a barrier behind every wave's drain
     vm_wait<0>();
     __syncthreads();
-  } else if constexpr (DEPTH == 5) {
-    // Ping-pong over a 3-buffer LDS-DMA ring (8-wave blocks, one per CU). Every wave
-    // alternates a LOAD segment (the fragment ds_reads of tile k into registers, then its
-    // share of tile k+2's LDS-DMA) and a COMPUTE segment (tile k's MFMAs on those
-    // registers), one raw barrier between segments. Waves 4-7 run one segment behind waves
-    // 0-3, so on every SIMD one wave's MFMAs overlap its partner's LDS reads and DMA issue
-    // instead of all 8 waves contending for the LDS in lockstep and then for the matrix
-    // pipe (cdna_hip_programming.md §5 8-phase template, T3/T4: counted vmcnt, raw
-    // s_barrier, never a vmcnt(0) drain in the loop).
-    // Ordering (segment s = one barrier interval; group 0 loads tile k in s = 2k, group 1
-    // in 2k+1): RAW — a wave retires its own DMAs of tile k+1 with the counted vmcnt at
-    // the end of its load segment k, before a barrier every reader of tile k+1 has passed
-    // (group 0 reads it in 2k+2, group 1 in 2k+3). WAR — tile k+2 overwrites the buffer of
-    // tile k-1, which group 1 last read in segment 2k-1 and retired (lgkmcnt(0)) before the
-    // barrier ending it; group 0's DMA issue is in segment 2k. Past-the-end tiles are not
-    // issued, so the last two load segments drain the queue (vmcnt(0)).
-    static_assert(NT == 512, "ping-pong needs two 4-wave groups");
-    constexpr int NL = T::A_CH + T::B_CH;   // LDS-DMA instructions per wave per tile
-    const bool late = wvu >= 4;
-    issue_glds(k_begin, 0);
-    issue_glds(k_begin + BK, 1);
-    vm_wait<NL>();
-    lds_barrier();
-    if (late) lds_barrier();
-    stamp(1);
-    int buf = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-      bf16x8 af[2][TM], bfr[2][TN];
-      if (p.ablate & 8) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) af[u][i] = bf16x8{};
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[u][j] = bf16x8{};
-        }
-      } else {
-        read_frags(buf, af, bfr);
-      }
-      const bool more = kt + 2 < nk;
-      if (more) issue_glds(k_begin + (kt + 2) * BK, buf == 0 ? 2 : buf - 1);
-      // retire this wave's DMAs of tile k+1 before the barrier: group 0 reads that tile in
-      // the very next segment (a wait placed after the MFMAs would be too late for group 1's
-      // share, which group 0 reads during group 1's compute segment)
-      if (more) vm_wait<NL>(); else vm_wait<0>();
-      if (kt < 160) stamp(2 + 3 * kt);
-      lds_barrier();
-      if (kt < 160) stamp(3 + 3 * kt);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-      if (!(p.ablate & 4)) mfma_tile(af, bfr);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt < 160) stamp(4 + 3 * kt);
-      __builtin_amdgcn_s_barrier();
-      buf = buf == 2 ? 0 : buf + 1;
-    }
-    if (!late) __builtin_amdgcn_s_barrier();
-  } else if (DEPTH == 4) {
-    // 3-buffer LDS-DMA ring: tile k+2's DMA is issued while tile k computes. The counted
-    // vmcnt before each raw barrier retires only tile k; tile k+1 stays in flight across
-    // it (a __syncthreads() would drain every DMA: its fence waits vmcnt(0)). The buffer
-    // refilled after the barrier held tile k-1, whose reads every wave finished before
-    // arriving there. Past-the-end tiles load the zero page, so any nk is safe.
-    constexpr int NL = T::A_CH + T::B_CH;   // global_load_lds per wave per tile
-    issue_glds(k_begin, 0);
-    issue_glds(k_begin + BK, 1);
-    int buf = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) vm_wait<NL>(); else vm_wait<0>();
-      lds_barrier();
-      if (kt + 2 < nk) issue_glds(k_begin + (kt + 2) * BK, buf == 0 ? 2 : buf - 1);
-      compute(buf);
-      buf = buf == 2 ? 0 : buf + 1;
-    }
-    __syncthreads();
-  } else if (DEPTH == 3) {
+  } else if constexpr (DEPTH == 3) {
     // the DMA of tile k+1 overlaps the MFMAs of tile k; the barrier's vmcnt(0) lands it
     if (nk > 0) issue_glds(k_begin, 0);
     __syncthreads();
+    stamp(1);
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
       if (kt + 1 < nk) issue_glds(k_begin + (kt + 1) * BK, buf ^ 1);
@@ -1667,7 +1450,6 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
     __syncthreads();   // C-tile reads of the store loop are done
     float* red = reinterpret_cast<float*>(smem);   // [NT/64][3][BN]
     static_assert((NT / 64) * 3 * BN * 4 <= LDS, "BN-bwd stat reduction must fit the staging LDS");
-    static_assert(!SF || 16 + (NT / BN) * 3 * BN * 8 <= LDS, "StatFuse tail scratch must fit the staging LDS");
     if (lane < CPR) {
 #pragma unroll
       for (int k = 0; k < 3; ++k)
@@ -1681,14 +1463,8 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
 #pragma unroll
       for (int w2 = 0; w2 < NT / 64; ++w2) s += red[(w2 * 3 + k) * BN + col];
       if (n0 + col < p.Ncol) {
-        float* dst = p.bs.slab + ((size_t)(p.bs.row0 + mt) * bs_ns + k) * p.Ncol + n0 + col;
-        if constexpr (SF) st_sc1(dst, s);
-        else *dst = s;
+        p.bs.slab[((size_t)(p.bs.row0 + mt) * bs_ns + k) * p.Ncol + n0 + col] = s;
       }
-    }
-    if constexpr (SF) {
-      if (bs_ns == 3) stat_fuse_tail<NT, BN, 3>(p.sf, p.bs.slab, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
-      else stat_fuse_tail<NT, BN, 2>(p.sf, p.bs.slab, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
     }
   }
 
@@ -1729,12 +1505,9 @@ __global__ __launch_bounds__(64 * WM * WN, (igemm_min_waves<MODE, BM, BN, WM, WN
 #pragma unroll
       for (int w2 = 0; w2 < WM; ++w2) s += red[(w2 * 2 + which) * BN + col];
       if (n0 + col < p.Ncol) {
-        float* dst = p.stats + ((size_t)mt * 2 + which) * p.Ncol + n0 + col;
-        if constexpr (SF) st_sc1(dst, s);
-        else *dst = s;
+        p.stats[((size_t)mt * 2 + which) * p.Ncol + n0 + col] = s;
       }
     }
-    if constexpr (SF) stat_fuse_tail<NT, BN, 2>(p.sf, p.stats, p.Ncol, mt, p.m_tiles, nt, p.n_tiles, n0, smem);
   }
   stamp(kTraceSlots - 2);
   if (trace_on)
@@ -1817,25 +1590,6 @@ int igemm_ablate() {
   return a;
 }
 
-// 3-buffer LDS-DMA ring for FWD/DGRAD GEMMs of more than two K-tiles (SDX_IGEMM_RING=1)
-int igemm_ring() {
-  static const int v = [] {
-    const char* e = getenv("SDX_IGEMM_RING");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// main loop of the 8-wave 256x128 / 128x256 tiles: 0 DEPTH 3, 1 ping-pong (DEPTH 5), 2 in-wave
-// pipelined (DEPTH 6, default)
-int igemm_pp() {
-  static const int v = [] {
-    const char* e = getenv("SDX_IGEMM_PP");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-
 int igemm_worder() {
   static const int v = [] {
     const char* e = getenv("SDX_WGRAD_ORDER");
@@ -1869,9 +1623,9 @@ hipError_t launch_v(bool one, int grid, const IgemmParams& p, hipStream_t s) {
 
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
-  // LDS-DMA main loops (DEPTH 3: two buffers; 5: ping-pong ring) carry every epilogue
-  // variant; the single-stage (ONE) form is DEPTH 3 at one K-tile
-  constexpr bool GLK = (DEPTH == 3 || DEPTH >= 5) && MODE != MODE_WGRAD;
+  // LDS-DMA main loops (DEPTH 3: two buffers; 6: in-wave pipelined ring; 7 / 8: tap reuse)
+  // carry every epilogue variant; the single-stage (ONE) form is DEPTH 3 at one K-tile
+  constexpr bool GLK = (DEPTH == 3 || DEPTH >= 6) && MODE != MODE_WGRAD;
   const bool one = DEPTH == 3 && p.Kdim <= BK && igemm_one();
   if (MODE == MODE_FWD && p.bn_sc != nullptr) {
     // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
@@ -1881,15 +1635,6 @@ hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   if (bs && p.bs.store_masked) {
     // masked-store statistics variant (projection head, BN3 fold): LDS-DMA tiles only
     if constexpr (MODE == MODE_DGRAD && GLK) return launch_v<MODE, BM, BN, WM, WN, DEPTH, 2>(one, grid, p, s);
-    return hipErrorInvalidValue;
-  }
-  if (p.sf.cnt != nullptr) {
-    // in-kernel statistics reduction: LDS-DMA variants only (launch_cfg routes here)
-    if constexpr (GLK) {
-      constexpr int V = MODE == MODE_DGRAD ? 3 : 1;
-      if (MODE == MODE_DGRAD && !bs) return hipErrorInvalidValue;
-      return launch_v<MODE, BM, BN, WM, WN, DEPTH, V>(one, grid, p, s);
-    }
     return hipErrorInvalidValue;
   }
   if constexpr (MODE == MODE_DGRAD) {
@@ -1936,9 +1681,6 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
     grid = most * p.ncls;
     if (grid == 0) return hipSuccess;
   }
-  if (p.sf.cnt != nullptr &&
-      (MODE == MODE_WGRAD || p.sf.group < 1 || p.sf.n_groups != (p.m_tiles + p.sf.group - 1) / p.sf.group))
-    return hipErrorInvalidValue;   // the plan must match this tile config (stat_fuse_groups)
   if constexpr (MODE == MODE_WGRAD) {
     const ConvGeom& g = p.g;
     const bool k1 = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
@@ -1951,38 +1693,15 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
   constexpr bool kDepth2 = (BM == 64 && BN == 64) || (MODE == MODE_FWD && BM != 256);
   const bool bs = MODE == MODE_DGRAD && p.bs.slab != nullptr;
   {
-    // WGRAD keeps register staging by default: measured 1-9% slower with LDS-DMA
-    // (SDX_IGEMM_GLDS=2 enables it there too)
-    // 256x128 / 128x256 tiles at more than two K-tiles: the 8-wave ones run the ping-pong
-    // loop (DEPTH 5, SDX_IGEMM_PP=1) or the in-wave pipelined loop (DEPTH 6, SDX_IGEMM_PP=2,
-    // default); the 4-wave ones (64x128 / 128x64 wave tiles) DEPTH 6
-    constexpr bool kPP = WM * WN == 8 && BM * BN == 256 * 128;
-    constexpr bool kW1 = BM * BN >= 128 * 256;
-    const bool pp = kPP && igemm_pp() == 1 && p.Kdim > 2 * BK && p.in_scale == nullptr;
-    // the channel dim of the K decode (FWD C, DGRAD K) a multiple of BK: branch-free advance
+    // 8-wave 256x128 / 128x256 tiles at more than two K-tiles whose channel dim (FWD C,
+    // DGRAD K) is a multiple of BK (branch-free K decode): the in-wave pipelined loop (DEPTH 6)
+    constexpr bool kW1 = WM * WN == 8 && BM * BN == 256 * 128;
     const int cdim_h = MODE == MODE_FWD ? p.g.C : p.g.K;
     const int taps_h = MODE == MODE_FWD ? p.g.R * p.g.S : p.nr * p.ns;
-    const bool w1 = kW1 && (WM * WN == 4 || igemm_pp() == 2) && p.Kdim > 2 * BK && p.in_scale == nullptr &&
-                    cdim_h % BK == 0 && taps_h <= 32;
-    if (p.sf.cnt != nullptr) {
-      if (p.in_scale != nullptr) return hipErrorInvalidValue;
-      if constexpr (kPP) {
-        if (pp) return launch_k<MODE, BM, BN, WM, WN, 5>(bs, grid, p, s);
-      }
-      if constexpr (kW1 && MODE != MODE_WGRAD) {
+    const bool w1 = kW1 && p.Kdim > 2 * BK && p.in_scale == nullptr && cdim_h % BK == 0 && taps_h <= 32;
+    if (p.in_scale == nullptr && igemm_glds() != 0) {
+      if constexpr (kW1) {
         if (w1) return launch_k<MODE, BM, BN, WM, WN, 6>(bs, grid, p, s);
-      }
-      return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
-    }
-    if (p.in_scale == nullptr && (MODE == MODE_WGRAD ? igemm_glds() == 2 : igemm_glds() != 0)) {
-      if constexpr (kPP) {
-        if (pp) return launch_k<MODE, BM, BN, WM, WN, 5>(bs, grid, p, s);
-      }
-      if constexpr (kW1 && MODE != MODE_WGRAD) {
-        if (w1) return launch_k<MODE, BM, BN, WM, WN, 6>(bs, grid, p, s);
-      }
-      if constexpr (MODE != MODE_WGRAD) {
-        if (igemm_ring() && p.Kdim > 2 * BK) return launch_k<MODE, BM, BN, WM, WN, 4>(bs, grid, p, s);
       }
       return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
     }
@@ -2030,7 +1749,7 @@ template <int MODE, int BM, int BN, int WM, int WN, int DEPTH>
 hipError_t launch_tap(IgemmParams p, hipStream_t s) {
   if (!tap_geom(p, BM, DEPTH, MODE)) return hipErrorInvalidValue;
   // the in-kernel statistics reduction and the BN+ReLU operand prologue are not built here
-  if (p.sf.cnt != nullptr || p.in_scale != nullptr) return hipErrorInvalidValue;
+  if (p.in_scale != nullptr) return hipErrorInvalidValue;
   p.ablate = igemm_ablate();
   p.trace = igemm_trace_on();
   p.m_tiles = (p.M + BM - 1) / BM;
@@ -2042,9 +1761,8 @@ hipError_t launch_tap(IgemmParams p, hipStream_t s) {
 // tile configs: 0 128x128 (2x2 waves of 64x64), 1 256x64 (4x1), 2 64x256 (1x4), 3 64x64 (2x2 waves of 32x32),
 // 4 128x128 with 8 waves (2x4 of 64x32: twice the waves per SIMD for latency hiding),
 // 5 256x128 with 8 waves (4x2 of 64x64, one block per CU), 6 128x256 with 8 waves (2x4 of
-// 64x64); both run the ping-pong main loop (DEPTH 5, 144 KiB LDS ring) at K > 128;
-// 7 128x256 / 8 256x128 with 4 waves (2x2 of 64x128 / 128x64, one wave per SIMD), the in-wave
-// pipelined loop (DEPTH 6) at K > 128
+// 64x64); both run the in-wave pipelined loop (DEPTH 6, 144 KiB LDS ring) at K > 128.
+// (7 / 8, 4-wave 64x128 wave tiles, measured slower than 5 / 6 in round 4 and removed.)
 template <int MODE>
 hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
   switch (cfg) {
@@ -2055,8 +1773,6 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
     case 4: return launch_cfg<MODE, 128, 128, 2, 4>(p, s);
     case 5: return launch_cfg<MODE, 256, 128, 4, 2>(p, s);
     case 6: return launch_cfg<MODE, 128, 256, 2, 4>(p, s);
-    case 7: return launch_cfg<MODE, 128, 256, 2, 2>(p, s);
-    case 8: return launch_cfg<MODE, 256, 128, 2, 2>(p, s);
     // tap-reuse 3x3 (FWD / stride-1 DGRAD only): 11 256x64 with 4 waves of 64x64 and one halo
     // buffer (C = 64: two blocks per CU), 12 256x128 with 8 waves (4x2 of 64x64), 13 128x128
     // with 8 waves (2x4 of 64x32)
@@ -2076,11 +1792,11 @@ hipError_t launch_any(IgemmParams p, int cfg, hipStream_t s) {
 }  // namespace
 
 int igemm_tile_m(int cfg) {
-  static const int m[14] = {128, 256, 64, 64, 128, 256, 128, 128, 256, 0, 0, 256, 256, 128};
+  static const int m[14] = {128, 256, 64, 64, 128, 256, 128, 0, 0, 0, 0, 256, 256, 128};
   return (cfg >= 0 && cfg < 14) ? m[cfg] : 0;
 }
 int igemm_tile_n(int cfg) {
-  static const int n[14] = {128, 64, 256, 64, 128, 128, 256, 256, 128, 0, 0, 64, 128, 128};
+  static const int n[14] = {128, 64, 256, 64, 128, 128, 256, 0, 0, 0, 0, 64, 128, 128};
   return (cfg >= 0 && cfg < 14) ? n[cfg] : 0;
 }
 
@@ -2113,14 +1829,9 @@ void set_epi(IgemmParams& p, const GemmEpi* epi) {
 }  // namespace
 
 hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void* y, float* stats, int cfg,
-                           hipStream_t s, const float* in_scale, const float* in_shift, const GemmEpi* epi,
-                           const StatFuse* sf) {
+                           hipStream_t s, const float* in_scale, const float* in_shift, const GemmEpi* epi) {
   IgemmParams p{};
   set_epi(p, epi);
-  if (sf != nullptr) {
-    if (stats == nullptr) return hipErrorInvalidValue;
-    p.sf = *sf;
-  }
   if (p.out_f32 && stats != nullptr) return hipErrorInvalidValue;
   // BN-apply epilogue: stride-1 1x1 geometry (the residual shares the output rows), no
   // statistics / fp32 output / bias; statistics-only pass: y == nullptr needs stats
@@ -2167,14 +1878,8 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
 
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
-                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi,
-                                   const StatFuse* sf) {
+                                   const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi) {
   IgemmParams p{};
-  if (sf != nullptr) {
-    // a single-launch dgrad only (a strided dgrad's classes fill one slab in several launches)
-    if (bstat == nullptr || bstat->slab == nullptr || g.stride != 1 || bstat->row0 != 0) return hipErrorInvalidValue;
-    p.sf = *sf;
-  }
   set_epi(p, epi);
   if (p.out_f32 && (g.stride != 1 || addend != nullptr || (bstat != nullptr && bstat->slab != nullptr)))
     return hipErrorInvalidValue;
@@ -2259,17 +1964,6 @@ hipError_t launch_conv_dgrad_merged(const ConvGeom& g, const void* dy, const voi
   p.Kdim = maxk;
   (void)maxt;
   return launch_any<MODE_DGRAD>(p, cfg, s);
-}
-
-int stat_fuse_groups(int m_tiles) {
-  int g = 1;
-  while (g * g < m_tiles) ++g;   // ~sqrt: level-1 and level-2 reductions of similar length
-  return g;
-}
-
-int stat_fuse_counters(int m_tiles, int n_tiles) {
-  const int g = stat_fuse_groups(m_tiles);
-  return ((m_tiles + g - 1) / g + 1) * n_tiles;
 }
 
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits) {
@@ -2430,9 +2124,8 @@ hipError_t launch_splitk_reduce(const float* partial, int splits, long n4, float
   return hipSuccess;
 }
 
-// the BN-apply epilogue runs on the LDS-DMA tiles (DEPTH 3), not the register-staged or
-// ring variants
-bool conv_fwd_bnapply_supported() { return igemm_glds() != 0 && !igemm_ring(); }
+// the BN-apply epilogue runs on the LDS-DMA tiles, not the register-staged ones
+bool conv_fwd_bnapply_supported() { return igemm_glds() != 0; }
 
 // the diagnostic timeline of the last traced launch (SDX_IGEMM_TRACE=1): 2 x kTraceSlots u64
 int igemm_trace_slots() { return kTraceSlots; }

@@ -279,199 +279,6 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_kernel(W3Params p) {
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Fragment-pipelined variant (opt-in, SDX_W3_PIPE=1; measured 1-9 % SLOWER per dispatch than
-// the kernel above, step +0.05 ms: profiles/ablate_wgrad_r3.txt). Four waves,
-// one per SIMD, each owning all 64 output channels x 144 columns (4 x 9 accumulator tiles):
-// per 32-pixel step a wave reads 13 fragments for 36 MFMAs (the 8-wave kernel: 11 for 18),
-// so the LDS fragment traffic per step drops from 88 to 52 KB, and the 512-VGPR budget of a
-// lone wave holds a second fragment set. The schedule is wgrad1x1.hip's pipelined one: a
-// THREE-buffer LDS ring; iteration k reads step k+1's fragments, runs step k's MFMAs on the
-// fragments read during iteration k-1 and stores step k+2 from the register ring into the
-// buffer step k-1 vacated — one barrier per step, no fragment-read latency in front of the
-// MFMAs. Loads use 32-bit element offsets + a scalar step offset (host check: P·K, P·C <
-// 2^31) and select the zero page through an SGPR pair the compiler cannot rematerialise.
-constexpr int W3P_NT = 256;
-
-template <int W>
-__global__ __launch_bounds__(W3P_NT, 1) void wgrad3x3_pipe_kernel(W3Params p) {
-  using G = W3Geom<W>;
-  constexpr int RPS = G::RPS;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[3 * G::STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
-  const int h4 = lane >> 4, c16 = lane & 15;
-
-  const int tiles = p.k_tiles * p.c_tiles;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = lin % tiles, split = lin / tiles;
-  const int k0 = (tile / p.c_tiles) * 64, c0 = (tile % p.c_tiles) * 64;
-  const int s_begin = split * p.steps_per_split;
-  const int s_end = min(p.steps_total, s_begin + p.steps_per_split);
-
-  // zero the pad columns of the three x windows (never written by the loads)
-  for (int e = tid; e < 3 * 3 * RPS * 2 * 8; e += W3P_NT) {
-    const int ch = e & 7, side = (e >> 3) & 1, ri = (e >> 4) % (3 * RPS), buf = (e >> 4) / (3 * RPS);
-    const int row = ri * G::P + (side ? W + 1 : 0);
-    *reinterpret_cast<uint4*>(smem + buf * G::STAGE + W3_DY_BYTES + w3_off(row, ch)) = make_uint4(0u, 0u, 0u, 0u);
-  }
-
-  // loader: 1024 16-B chunks per step, 4 per thread: chunk 0 = dy chunk tid (pixel tid/8,
-  // channel chunk tid%8), chunks 1..3 = x-window chunks tid + 256·(u−1): channel chunk e%8
-  // of pixel w of window row ri = (tap row r, image row i) (as wgrad3x3_kernel)
-  struct XChunk {
-    int off;   // element offset of step 0 (may be negative: used only when valid)
-    int i, r, dst;
-  };
-  auto x_chunk = [&](int e) __attribute__((always_inline)) -> XChunk {
-    const int ch = e & 7, rest = e >> 3;
-    const int w = rest % W, ri = rest / W;
-    const int r = ri / RPS, i = ri % RPS;
-    return {((i + r - 1) * W + w) * p.C + c0 + ch * 8, i, r, W3_DY_BYTES + w3_off(ri * G::P + w + 1, ch)};
-  };
-  const XChunk x1 = x_chunk(tid), x2 = x_chunk(tid + 256), x3 = x_chunk(tid + 512);
-  const int dy_off = (tid >> 3) * p.K + k0 + (tid & 7) * 8;
-  const int dy_dst = w3_off(tid >> 3, tid & 7);
-  const int sA = 32 * p.K, sB = 32 * p.C;
-  w3_gptr zp = (w3_gptr)w3_zero16;
-  asm volatile("" : "+s"(zp));
-  const w3_gptr gdy = (w3_gptr)p.dy, gx = (w3_gptr)p.x;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef const __attribute__((address_space(1))) u32x4* g16;
-  auto x_src = [&](const XChunk& xc, int step) __attribute__((always_inline)) -> w3_gptr {
-    const int hs = ((step * RPS + xc.i) & (W - 1)) + xc.r - 1;   // H == W
-    const bool ok = step < s_end && (unsigned)hs < (unsigned)W;
-    return ok ? gx + (xc.off + step * sB) : zp;
-  };
-  struct Regs {
-    u32x4 a, b, c, d;
-  };
-  Regs r0, r1, r2, r3;
-  auto slot = [&](auto S) __attribute__((always_inline)) -> Regs& {
-    if constexpr (decltype(S)::value == 0) return r0;
-    else if constexpr (decltype(S)::value == 1) return r1;
-    else if constexpr (decltype(S)::value == 2) return r2;
-    else return r3;
-  };
-  auto load = [&](int step, Regs& r) __attribute__((always_inline)) {
-    r.a = *(g16)(step < s_end ? gdy + (dy_off + step * sA) : zp);
-    r.b = *(g16)x_src(x1, step);
-    r.c = *(g16)x_src(x2, step);
-    r.d = *(g16)x_src(x3, step);
-  };
-  auto store = [&](unsigned char* sb, const Regs& r) __attribute__((always_inline)) {
-    *reinterpret_cast<u32x4*>(sb + dy_dst) = r.a;
-    *reinterpret_cast<u32x4*>(sb + x1.dst) = r.b;
-    *reinterpret_cast<u32x4*>(sb + x2.dst) = r.c;
-    *reinterpret_cast<u32x4*>(sb + x3.dst) = r.d;
-  };
-
-  // fragment offsets (step-invariant, as wgrad3x3_kernel; A: all 64 output channels)
-  const int q = c16 >> 2, pp = c16 & 3;
-  const int p_lo = 8 * h4 + q, p_hi = p_lo + 4;
-  const int xb_lo = (p_lo / W) * G::P + (p_lo % W);
-  const int xb_hi = (p_hi / W) * G::P + (p_hi % W);
-  auto lane_off = [&](int row, int col0) __attribute__((always_inline)) {
-    const int col = col0 + 4 * pp;
-    return w3_off(row, col >> 3) + (col & 7) * 2;
-  };
-  int ao_lo[4], ao_hi[4], bo_lo[9], bo_hi[9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    ao_lo[i] = lane_off(p_lo, 16 * i);
-    ao_hi[i] = lane_off(p_hi, 16 * i);
-  }
-#pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    const int n = wn * 144 + 16 * j;
-    const int t = n >> 6, r = t / 3, s = t - 3 * r;
-    const int off = r * RPS * G::P + s;
-    bo_lo[j] = W3_DY_BYTES + lane_off(xb_lo + off, n & 63);
-    bo_hi[j] = W3_DY_BYTES + lane_off(xb_hi + off, n & 63);
-  }
-  auto frag = [&](const unsigned char* base, int o_lo, int o_hi) __attribute__((always_inline)) -> bf16x8 {
-    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_lo));
-    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_bf16x4*)(base + o_hi));
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-
-  f32x4 acc[4][9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 fa0[4], fb0[9], fa1[4], fb1[9];
-  auto read_frags = [&](const unsigned char* base, bf16x8 (&fa)[4], bf16x8 (&fb)[9]) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) fb[j] = frag(base, bo_lo[j], bo_hi[j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = frag(base, ao_lo[i], ao_hi[i]);
-  };
-  auto mfmas = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[9]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 9; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-  };
-
-  unsigned char* b_cur = smem;
-  unsigned char* b_nxt = smem + G::STAGE;
-  unsigned char* b_st = smem + 2 * G::STAGE;
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  auto iter = [&](int b0, auto U) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-    using S = std::integral_constant<int, (u + 2) % 4>;
-    if constexpr ((u & 1) == 0) {
-      read_frags(b_nxt, fa1, fb1);
-      mfmas(fa0, fb0);
-    } else {
-      read_frags(b_nxt, fa0, fb0);
-      mfmas(fa1, fb1);
-    }
-    store(b_st, slot(S{}));
-    load(b0 + u + 6, slot(S{}));
-    __syncthreads();
-    unsigned char* t = b_cur;
-    b_cur = b_nxt;
-    b_nxt = b_st;
-    b_st = t;
-  };
-  load(s_begin, r0);
-  load(s_begin + 1, r1);
-  load(s_begin + 2, r2);
-  load(s_begin + 3, r3);
-  store(b_cur, r0);
-  store(b_nxt, r1);
-  load(s_begin + 4, r0);
-  load(s_begin + 5, r1);
-  __syncthreads();
-  read_frags(b_cur, fa0, fb0);
-  for (int b0 = s_begin; b0 < s_end; b0 += 4) {
-    iter(b0, I0{});
-    iter(b0, I1{});
-    iter(b0, I2{});
-    iter(b0, I3{});
-  }
-
-  const int Ncol = 9 * p.C;
-  float* out = p.part + (size_t)split * p.K * Ncol;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = k0 + 16 * i + c16;
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int n = wn * 144 + 16 * j + 4 * h4;
-      const int t = n >> 6;
-      const f32x4 a = acc[i][j];
-      st16<SDX_NT_PART != 0>(out + (size_t)m * Ncol + t * p.C + c0 + (n & 63),
-                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
-                                        __float_as_uint(a[3])));
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // Stride-2 variant (the first 3x3 conv of layers 2-4, reference networks/resnet_big.py:45):
@@ -845,15 +652,6 @@ __global__ __launch_bounds__(W3_NT, 1) void wgrad3x3_pad_kernel(W3Params p) {
   }
 }
 
-bool w3_pipe_enabled(const ConvGeom& g) {
-  static const bool on = [] {
-    const char* e = getenv("SDX_W3_PIPE");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  const long P = (long)g.N * g.H * g.W;   // 32-bit element offsets
-  return on && P * g.K < (1L << 31) && P * g.C < (1L << 31);
-}
-
 // padded-slot kernel: slot width WS (next power of two >= W) for stride-1 widths that are not
 // one of {4, 8, 16, 32}
 int w3_pad_ws(const ConvGeom& g) {
@@ -954,14 +752,6 @@ hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, flo
         case 16: hipLaunchKernelGGL((wgrad3x3_s2_kernel<16, false>), grid, block, 0, s, p); break;
         default: hipLaunchKernelGGL((wgrad3x3_s2_kernel<32, false>), grid, block, 0, s, p); break;
       }
-    }
-  } else if (w3_pipe_enabled(g)) {
-    const dim3 pblock(W3P_NT);
-    switch (g.W) {
-      case 4: hipLaunchKernelGGL(wgrad3x3_pipe_kernel<4>, grid, pblock, 0, s, p); break;
-      case 8: hipLaunchKernelGGL(wgrad3x3_pipe_kernel<8>, grid, pblock, 0, s, p); break;
-      case 16: hipLaunchKernelGGL(wgrad3x3_pipe_kernel<16>, grid, pblock, 0, s, p); break;
-      default: hipLaunchKernelGGL(wgrad3x3_pipe_kernel<32>, grid, pblock, 0, s, p); break;
     }
   } else {
     switch (g.W) {

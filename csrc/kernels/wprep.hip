@@ -94,7 +94,25 @@ __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ ma
   }
 }
 
+// dst[r][c] += src[r][c] for c < C of a channel-padded [rows][Cp] fp32 weight gradient (the
+// stem's 3 input channels are padded to 8 for its conv kernels): the fp32 gradient sink keeps
+// the unpadded [K][R][S][C] layout
+__global__ __launch_bounds__(256) void unpad_add_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                        int rows, int Cp, int C) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * C) return;
+  const int r = e / C, c = e - r * C;
+  dst[e] += src[(long)r * Cp + c];
+}
+
 }  // namespace
+
+hipError_t launch_unpad_add(const float* src, float* dst, int rows, int Cp, int C, hipStream_t s) {
+  if (rows < 1 || C < 1 || C > Cp) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(unpad_add_kernel, dim3((rows * C + 255) / 256), dim3(256), 0, s, src, dst, rows, Cp, C);
+  SDX_LAUNCH_CHECK();
+  return hipSuccess;
+}
 
 hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s) {
   // `total` = the largest conv's tile count (ceil(K/64)·ceil(Cp/64)·R·S), computed by the host

@@ -173,6 +173,8 @@ class PretrainEngine:
         self.record_norm_mean = torch.zeros((), device=dev)
         self._rnm_valid = torch.zeros((), device=dev)
         self._seed_t = torch.zeros((1,), dtype=torch.int64, device=dev)
+        self._seed_host = 0
+        self._seed_dev = False     # True once a hipGraph of the step exists (the seed then lives in _seed_t)
         self._ramp_t = torch.zeros((), device=dev)
         self._graph = None
         self._graph_stats = None
@@ -268,6 +270,7 @@ class PretrainEngine:
         if getattr(self.optimizer, "norms", None) is not None:
             state.append(self.optimizer.norms)
         snap = [t.detach().clone() for t in state]
+        pend = self.runner._nbt_pending
         active = self.syncbn_transport
         group = self.runner.sync_group
         self._host_prelude(1, 0, 1)
@@ -290,6 +293,7 @@ class PretrainEngine:
         with torch.no_grad():
             for t, v in zip(state, snap):
                 t.copy_(v)
+        self.runner._nbt_pending = pend
         for item in filter(None, os.environ.get("SDX_SYNCBN_TUNE_SKEW", "").split(",")):
             r, nm, extra = item.split(":")
             if int(r) == self.rank and nm in names:
@@ -345,7 +349,9 @@ class PretrainEngine:
             return self._make_views_cpu(idx, epoch, it)
         if self.backend == "native":
             # the seed is read from device memory by the kernel (graph-replay safe)
-            x = augment_gpu(self.data, idx, self.aug, 0, self._seed_t, self.data_offs, self.data_hw)
+            # eager: the seed is a kernel argument; a captured step reads it from _seed_t at replay
+            x = augment_gpu(self.data, idx, self.aug, self._seed_host, self._seed_t if self._seed_dev else None,
+                            self.data_offs, self.data_hw)
         else:
             x = augment(self.data, idx, self.aug, step_seed(self.opt.seed, epoch, it, self.rank), self.data_offs,
                         self.data_hw)
@@ -371,7 +377,9 @@ class PretrainEngine:
         opt = self.opt
         warmup_learning_rate(opt, epoch, it, iters, self.optimizer)
         self.optimizer._sync_lr()
-        self._seed_t.fill_(step_seed(opt.seed, epoch, it, self.rank))
+        self._seed_host = step_seed(opt.seed, epoch, it, self.rank)
+        if self._seed_dev:
+            self._seed_t.fill_(self._seed_host)
         if opt.sec or opt.l2reg:
             now_iter = (epoch - 1) * iters + it
             self._ramp_t.fill_(now_iter / (opt.epochs * iters))
@@ -438,6 +446,7 @@ class PretrainEngine:
         bns = [m for m in self.model.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
         saved = [(m.running_mean.clone(), m.running_var.clone(), m.num_batches_tracked.clone())
                  for m in bns if m.running_mean is not None]
+        pend = self.runner._nbt_pending
         with ph("forward"), torch.no_grad():
             feats = torch.cat([self.runner.forward(c) for c in chunks])
         with torch.no_grad():          # undo the statistics updates of the no-grad pass
@@ -445,6 +454,7 @@ class PretrainEngine:
                 m.running_mean.copy_(rm)
                 m.running_var.copy_(rv)
                 m.num_batches_tracked.copy_(nb)
+        self.runner._nbt_pending = pend
         feats = feats.detach().requires_grad_(True)
         with ph("loss"):
             loss = self.criterion(feats, labels if opt.method == "SupCon" else None)
@@ -479,6 +489,7 @@ class PretrainEngine:
         if self._graph is not None:
             self._idx_buf.copy_(idx, non_blocking=True)
             self._graph.replay()
+            self.runner._nbt_pending += self._graph_nbt
             st = self._graph_stats
         else:
             st = self._step_body(idx, epoch, it)
@@ -501,11 +512,13 @@ class PretrainEngine:
         if isinstance(self.sync_group, comm.EmulatedGroup):
             return False
         self._idx_buf = idx_example.clone()
+        self._seed_dev = True
         state = [self.flat.flat, self.optimizer.buf, self.record_norm_mean, self._rnm_valid]
         state += [t for t in self.model.buffers()]
         if getattr(self.optimizer, "norms", None) is not None:
             state.append(self.optimizer.norms)
         snap = [t.detach().clone() for t in state]
+        pend = self.runner._nbt_pending
         self._host_prelude(1, 0, 1)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
@@ -514,12 +527,18 @@ class PretrainEngine:
                 self._step_body(self._idx_buf)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        p0 = self.runner._nbt_pending
+        # thread-local capture: the communicator watchdog thread (csrc/bindings/comm_ops.cpp)
+        # keeps polling its events while this thread captures
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._graph_stats = self._step_body(self._idx_buf)
+        # BN passes of one step, counted on the host (ModelRunner.flush_bn_counters) per replay
+        self._graph_nbt = self.runner._nbt_pending - p0
         self._graph = g
         with torch.no_grad():
             for t, v in zip(state, snap):
                 t.copy_(v)
+        self.runner._nbt_pending = pend
         return True
 
     def _norm_terms(self, feats):

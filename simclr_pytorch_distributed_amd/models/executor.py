@@ -113,6 +113,12 @@ class ModelRunner:
         self.fused = fused
         self._wc = None
         self._nbt = None
+        # BatchNorm num_batches_tracked of the fused path: counted on the host and added to the
+        # buffers when something reads them (state_dict: checkpoints, evaluation copies) — no
+        # per-step kernel for a counter the training math never reads (momentum is set)
+        self._nbt_pending = 0
+        if hasattr(model, "register_state_dict_pre_hook"):
+            model.register_state_dict_pre_hook(lambda *a, **k: self.flush_bn_counters())
 
     def weight_cache(self):
         if self._wc is None:
@@ -147,8 +153,14 @@ class ModelRunner:
             out = fb.bottleneck(out, blk, wc, training, g, chain, next_native=i + 1 < len(blocks)) \
                 if isinstance(blk, Bottleneck) else fb.basic(out, blk, wc, training, g, chain)
         if training and self._nbt:
-            torch._foreach_add_(self._nbt, 1)
+            self._nbt_pending += 1
         return global_avgpool_nhwc(out)
+
+    def flush_bn_counters(self):
+        """Add the host-counted training passes to every BN's num_batches_tracked."""
+        if self._nbt_pending and self._nbt:
+            torch._foreach_add_(self._nbt, self._nbt_pending)
+        self._nbt_pending = 0
 
     def encode(self, x, training=None):
         enc = self.model.encoder

@@ -283,7 +283,11 @@ class _Stem(torch.autograd.Function):
         g = sinks.target(w)
         with SideWork(dy, x):
             dwk = m.conv_wgrad(dy, x, R, S, st, pad, 0, -1)      # [K][R][S][Cp] fp32
-            g.add_(dwk[..., :C].permute(0, 3, 1, 2))
+            gk = g.permute(0, 2, 3, 1)                             # [K][R][S][C] (channels_last sink)
+            if gk.is_contiguous():
+                m.unpad_add(dwk, gk)
+            else:
+                gk.add_(dwk[..., :C])
         sinks.notify(ctx.params)
         return (None, None, None, None, None) + (None,) * len(ctx.params)
 
