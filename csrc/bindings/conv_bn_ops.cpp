@@ -79,12 +79,35 @@ std::atomic<int>& tap3_flag() {
 // runtime switch of the tap-reuse loop (tests / in-process A/B); returns the previous value
 int64_t tap3_set(int64_t on) { return tap3_flag().exchange((int)on); }
 
-int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, bool plain) {
+//
+// Then per-pass corrections to auto_cfg from the round-5 re-calibration (every fwd / dgrad
+// of the CIFAR ResNet-50 at 512 views under every tile config, the dgrads with their
+// BN-statistics epilogue: tools/cfg_sweep.py, profiles/cfg_sweep_r5.txt; 5.32 -> 5.24 ms
+// summed stand-alone). Three corrections won stand-alone; in the step (bench A/B, same box,
+// SDX_CFG_RULES bit mask) only bit 4 does, so it alone is on by default:
+//  1 the 128x256 DEPTH-6 tile only when it fills the chip (>= 256 tiles): l4 1x1 / strided
+//    3x3 fwd at M = 8192 on the 8-wave 128x128 (52.8 vs 58.1 us) — neutral in the step;
+//  2 expanding stride-1 dgrads (dx has >= 256 and >= twice the reduction's channels) on the
+//    64x256 tile (l1 137.8 vs 146.3 us) — +0.05 ms in the step (12.21 vs 12.155 ms): more
+//    blocks per CU under the heavy epilogue is exactly what the side-stream wgrads lose;
+//  4 strided dgrads with 256-multiple outputs on DEPTH 6 (l3.0 3x3 84.4 vs 90.4 us, l3.0
+//    shortcut 127.3 vs 135.9) — -0.03 ms in the step (12.12 vs 12.155)
+int conv_cfg(const ConvGeom& g, int cdim, int ncol, int64_t M, int64_t Kdim, bool plain, bool dgrad) {
   if (tap3_flag().load(std::memory_order_relaxed) > 0 && plain && pinned_cfg() < 0) {
     const int t = igemm_tap_cfg(g, cdim, ncol);
     if (t >= 0) return t;
   }
-  return auto_cfg(M, ncol, Kdim, true);
+  int cfg = auto_cfg(M, ncol, Kdim, true);
+  static const int rules = [] {   // SDX_CFG_RULES: bit mask of the corrections below (A/B)
+    const char* e = getenv("SDX_CFG_RULES");
+    return e == nullptr ? 4 : atoi(e);
+  }();
+  if (pinned_cfg() >= 0) return cfg;
+  auto tiles = [&](int c) { return ((M + igemm_tile_m(c) - 1) / igemm_tile_m(c)) * ((ncol + igemm_tile_n(c) - 1) / igemm_tile_n(c)); };
+  if ((rules & 1) && cfg == 6 && tiles(6) < 256) cfg = 4;
+  if ((rules & 2) && dgrad && g.stride == 1 && ncol >= 256 && 2 * Kdim <= ncol) cfg = 2;
+  if ((rules & 4) && dgrad && g.stride > 1 && ncol % 256 == 0 && Kdim * g.stride * g.stride >= 1024) cfg = 6;
+  return cfg;
 }
 
 int auto_cfg(int64_t M, int64_t Ncol, int64_t Kdim, bool fill) {
@@ -145,7 +168,7 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
   c10::DeviceGuard dg(x.device());
   const int64_t M = (int64_t)g.N * g.P * g.Q;
   if (cfg < 0)
-    cfg = conv_cfg(g, g.C, g.K, M, (int64_t)g.R * g.S * g.C, !in_scale.has_value());
+    cfg = conv_cfg(g, g.C, g.K, M, (int64_t)g.R * g.S * g.C, !in_scale.has_value(), false);
   TORCH_CHECK(!no_out || (want_stats && epi == nullptr), "statistics-only conv: stats, no epilogue");
   auto y = no_out ? torch::Tensor() : torch::empty({g.N, g.P, g.Q, g.K}, x.options());
   torch::Tensor slab;
@@ -214,7 +237,7 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
   c10::DeviceGuard dg(dy.device());
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true, true);
   torch::Tensor dx;
   if (out.has_value()) {
     dx = *out;
@@ -307,15 +330,14 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
     check_bf16_nhwc(ya, "ya");
     TORCH_CHECK(ya.size(0) == dy.size(0) && ya.size(1) == H && ya.size(2) == W && ya.size(3) == C, "ya shape");
   }
-  TORCH_CHECK(extra_rows >= 0 && (!no_y || (!yb.has_value() && !msc.has_value())),
-              "no-ya statistics: no second BN input, ReLU mask from bits");
+  TORCH_CHECK(extra_rows >= 0 && (!no_y || !msc.has_value()), "no-ya statistics: ReLU mask from bits");
   check_vec(ma, C, "ma");
   BnBwdStat bs{};
   bs.ya = no_y ? nullptr : ya.data_ptr();
   bs.ma = ma.data_ptr<float>();
   if (yb.has_value()) {
     check_bf16_nhwc(*yb, "yb");
-    TORCH_CHECK(yb->sizes() == ya.sizes(), "yb shape");
+    TORCH_CHECK(yb->size(0) == dy.size(0) && yb->size(1) == H && yb->size(2) == W && yb->size(3) == C, "yb shape");
     TORCH_CHECK(mb.has_value(), "mb required with yb");
     check_vec(*mb, C, "mb");
     bs.yb = yb->data_ptr();
@@ -338,7 +360,7 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   g.C = C; g.R = wt.size(1); g.S = wt.size(2);
   g.H = H; g.W = W; g.stride = stride; g.pad = pad;
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true, true);
   int rows = 0;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) rows += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
@@ -1226,11 +1248,13 @@ std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor&
 // returns [out, y1, a1, y2, a2|-, y3|-, ys|-, omask (uint8 ReLU bits of out; training only),
 //          then sc, sh, mu, iv per BN]
 //
-// fold_fwd (identity bottleneck, training; ops/block.py decides): the forward half of the BN3
-// fold — conv3 runs twice, first for its BN statistics only (nothing stored), then with the
-// BN3 apply + residual + ReLU + output bits in its epilogue, so y3 is never written nor
-// re-read (≈2 passes over the block's widest tensor); its backward takes Σdz·y3 from
-// W3 and dzᵀ·a2 (block_bwd, bnfold_rowdot) instead of re-reading y3
+// fold_fwd (bottleneck, training; ops/block.py decides): the forward half of the BN3 fold —
+// conv3 runs twice, first for its BN statistics only (nothing stored), then with the BN3
+// apply + residual + ReLU + output bits in its epilogue, so y3 is never written nor re-read
+// (≈2 passes over the block's widest tensor); its backward takes Σdz·y3 from W3 and dzᵀ·a2
+// (block_bwd, bnfold_rowdot) instead of re-reading y3. Projection blocks: the residual is the
+// shortcut's pre-BN output with the shortcut BN applied in the same epilogue (that BN's
+// statistics are final before pass 2), which replaces the separate two-input apply pass
 //
 // side (optional HIP stream): a projection block's shortcut conv (+ its statistics slab) runs
 // there, concurrently with the main branch conv1 -> bn1 -> conv2 -> ...; its BN finalize (and
@@ -1281,9 +1305,25 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   st.push_back(c2.second);
   torch::Tensor last = c2.first, a2;
   int lastbn = 1;
-  fold_fwd = fold_fwd && bottleneck && !proj && training && stride == 1 && w[2].size(1) == 1 &&
-             w[2].size(2) == 1 && w[2].size(0) == x.size(3) && conv_fwd_bnapply_supported();
+  // identity blocks: the residual is x (stride 1, same width); projection blocks: the
+  // shortcut's pre-BN output ys, normalised in the same epilogue
+  fold_fwd = fold_fwd && bottleneck && training && w[2].size(1) == 1 && w[2].size(2) == 1 &&
+             (proj || (stride == 1 && w[2].size(0) == x.size(3))) && conv_fwd_bnapply_supported();
   torch::Tensor o, ys;
+  // the projection shortcut's output and BN statistics (joins the side stream if it ran there)
+  auto shortcut = [&] {
+    if (sc_done != nullptr) {
+      check_hip(hipStreamWaitEvent(cur_stream(), sc_done, 0), "hipStreamWaitEvent");
+      st.push_back(bn_forward(slab_side, rows_of(ys_side), B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps,
+                              momentum, training, comm));
+      ys = ys_side;
+    } else {
+      auto cs = conv_bn_fwd(x, w[nconv], stride, 0, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
+                            training, comm);
+      st.push_back(cs.second);
+      ys = cs.first;
+    }
+  };
   // the block output's ReLU mask for backward: 1 bit per element instead of re-reading out
   // (identity blocks: out has x's shape; projection / strided blocks: the last conv's)
   torch::Tensor omask;
@@ -1291,14 +1331,25 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
     a2 = bn_apply(c2.first, st[1].sc, st[1].sh, c10::nullopt, c10::nullopt, c10::nullopt, 0, true, c10::nullopt);
     if (fold_fwd) {
       // pass 1: BN3 statistics (nothing stored) -> finalize (SyncBN: fused exchange) ;
-      // pass 2: out = relu(bn3(y3) + x) and its bits straight from conv3's epilogue
+      // pass 2: out = relu(bn3(y3) + x) (projection: + bn_s(ys)) and its bits straight from
+      // conv3's epilogue
       auto c3s = conv_fwd_impl(a2, w[2], 1, 0, true, -1, c10::nullopt, c10::nullopt, nullptr, true);
       st.push_back(bn_forward(c3s[1], rows_of(a2), B(2, 0), B(2, 1), B(2, 2), B(2, 3), eps, momentum, training, comm));
-      omask = torch::empty({x.numel() / 8}, x.options().dtype(at::kByte));
       GemmEpi epi{};
       epi.bn_scale = st[2].sc.data_ptr<float>();
       epi.bn_shift = st[2].sh.data_ptr<float>();
-      epi.resid = x.data_ptr();
+      if (proj) {
+        shortcut();
+        TORCH_CHECK(ys.size(0) == a2.size(0) && ys.size(1) == a2.size(1) && ys.size(2) == a2.size(2) &&
+                        ys.size(3) == w[2].size(0),
+                    "block_fwd: shortcut output shape");
+        epi.resid = ys.data_ptr();
+        epi.resid_scale = st[3].sc.data_ptr<float>();
+        epi.resid_shift = st[3].sh.data_ptr<float>();
+      } else {
+        epi.resid = x.data_ptr();
+      }
+      omask = torch::empty({rows_of(a2) * w[2].size(0) / 8}, x.options().dtype(at::kByte));
       epi.mask_out = omask.data_ptr<uint8_t>();
       o = conv_fwd_impl(a2, w[2], 1, 0, false, -1, c10::nullopt, c10::nullopt, &epi)[0];
       last = torch::Tensor();
@@ -1315,17 +1366,7 @@ std::vector<torch::Tensor> block_fwd(torch::Tensor x, std::vector<torch::Tensor>
   if (fold_fwd) {
     // out computed by conv3's epilogue
   } else if (proj) {
-    if (sc_done != nullptr) {
-      check_hip(hipStreamWaitEvent(cur_stream(), sc_done, 0), "hipStreamWaitEvent");
-      st.push_back(bn_forward(slab_side, rows_of(ys_side), B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps,
-                              momentum, training, comm));
-      ys = ys_side;
-    } else {
-      auto cs = conv_bn_fwd(x, w[nconv], stride, 0, B(nconv, 0), B(nconv, 1), B(nconv, 2), B(nconv, 3), eps, momentum,
-                            training, comm);
-      st.push_back(cs.second);
-      ys = cs.first;
-    }
+    shortcut();
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, ys, st[nconv].sc, st[nconv].sh, 1, true, om);
   } else {
     o = bn_apply(last, st[lastbn].sc, st[lastbn].sh, x, c10::nullopt, c10::nullopt, 2, true, om);
@@ -1401,10 +1442,25 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
   const bool fold = bottleneck && have_slab && nfw >= 1 && nfw <= (proj ? 2u : 1u) && fold_w[0].defined() &&
                     (nfw == 1 || (stride == 1 && fold_w[1].defined()));
   const bool fold_sc = fold && proj && nfw == 2;
-  TORCH_CHECK(!no_y3 || (fold && !proj), "block_bwd: a forward-folded block needs its BN3 fold (next block's slab)");
+  TORCH_CHECK(!no_y3 || fold, "block_bwd: a forward-folded block needs its BN3 fold (next block's slab)");
   const torch::Tensor* gram3 = grams ? &fold_w[nfw] : nullptr;
   const torch::Tensor* grams_sc = grams && nfw == 2 ? &fold_w[nfw + 2] : nullptr;
   torch::Tensor coef3, coefs, Gfold;
+  if (no_y3) {
+    // Σdz·y3 = Σ_k W3[c][k]·(dzᵀ·a2)[c][k]: G on the main stream (the fold's wgrad reuses it),
+    // written into the two extra rows the next block's final dgrad left in in_slab (a
+    // projection block's third set, Σdz·(ys − μs), came from that dgrad's epilogue)
+    const int64_t C3 = dout.size(3), K3 = a2.size(3), ns = in_slab->size(1);
+    TORCH_CHECK(in_slab->size(0) > 2 && in_slab->size(2) == C3 && fold_w[0].size(0) == C3 &&
+                    fold_w[0].size(3) == K3,
+                "block_bwd: forward-folded BN3 slab / weights");
+    Gfold = torch::empty({C3, 1, 1, K3}, dout.options().dtype(at::kFloat));
+    conv_wgrad(dout, a2, 1, 1, 1, 0, 0, -1, Gfold, false, c10::nullopt, c10::nullopt);
+    float* rows = in_slab->data_ptr<float>() + (in_slab->size(0) - 2) * ns * C3;
+    check_hip(launch_bnfold_rowdot(Gfold.data_ptr<float>(), fold_w[0].data_ptr(), (int)C3, (int)K3, (int)ns, rows,
+                                   cur_stream()),
+              "bnfold_rowdot");
+  }
   if (proj) {
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), G(nconv, 0),
@@ -1426,20 +1482,6 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
       dys = r[1];
     }
   } else {
-    if (no_y3) {
-      // Σdz·y3 = Σ_k W3[c][k]·(dzᵀ·a2)[c][k]: G on the main stream (the fold's wgrad reuses it),
-      // written into the two extra rows the next block's final dgrad left in in_slab
-      const int64_t C3 = dout.size(3), K3 = a2.size(3);
-      TORCH_CHECK(in_slab->size(0) > 2 && in_slab->size(2) == C3 && fold_w[0].size(0) == C3 &&
-                      fold_w[0].size(3) == K3,
-                  "block_bwd: forward-folded BN3 slab / weights");
-      Gfold = torch::empty({C3, 1, 1, K3}, dout.options().dtype(at::kFloat));
-      conv_wgrad(dout, a2, 1, 1, 1, 0, 0, -1, Gfold, false, c10::nullopt, c10::nullopt);
-      float* rows = in_slab->data_ptr<float>() + (in_slab->size(0) - 2) * 2 * C3;
-      check_hip(launch_bnfold_rowdot(Gfold.data_ptr<float>(), fold_w[0].data_ptr(), (int)C3, (int)K3, rows,
-                                     cur_stream()),
-                "bnfold_rowdot");
-    }
     auto c = have_slab
                  ? bn_bwd_coef_slab(comm, *in_slab, cnt_last, G(lastbn, 0), S(lastbn, 2), S(lastbn, 3), c10::nullopt,
                                     c10::nullopt, c10::nullopt, G(lastbn, 1), G(lastbn, 2), c10::nullopt, c10::nullopt)
@@ -1514,7 +1556,7 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     // the previous block folded its BN3 forward too (no y3): Σdz and −μ·Σdz here, two slab
     // rows left for its Σdz·y3 (block_bwd no_y3)
     const bool prev_noy = !prev[0].defined() || prev[0].numel() == 0;
-    TORCH_CHECK(!prev_noy || (prev_fold && !two), "block_bwd: previous block without y3 must fold");
+    TORCH_CHECK(!prev_noy || prev_fold, "block_bwd: previous block without y3 must fold");
     auto r = conv_dgrad_bnstat(dy1, wt[0], H, W, s1, p1, -1, o, add, amask, prev[0], prev[1],
                                two ? OptT(prev[2]) : OptT(), two ? OptT(prev[3]) : OptT(), prev[4], c10::nullopt,
                                c10::nullopt, asub, prev_fold ? 1 : 0, prev_noy ? 2 : 0);

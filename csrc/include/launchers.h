@@ -47,8 +47,8 @@ hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S
                                const void* w, int C, int K, float* sink, int accumulate, hipStream_t s);
 // cs[K] = column sums of a [rows][K] bf16 tensor (partial: [bnfold_colsum_blocks()][K] scratch)
 int bnfold_colsum_blocks();
-// two BN-backward slab rows [2][2][C] carrying Σ_k W[c][k]·G[c][k] (fp64 as fp32 hi + lo) in set 1
-hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, float* out_rows, hipStream_t s);
+// two BN-backward slab rows [2][ns][C] carrying Σ_k W[c][k]·G[c][k] (fp64 as fp32 hi + lo) in set 1
+hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, int ns, float* out_rows, hipStream_t s);
 hipError_t launch_bnfold_colsum(const void* x, long rows, int K, float* partial, float* cs, hipStream_t s);
 
 // ---- implicit-GEMM convolution (igemm.hip) ------------------------------------
@@ -90,6 +90,10 @@ struct GemmEpi {
   const float* bn_shift;
   const void* resid;
   uint8_t* mask_out;
+  // projection blocks: resid is the shortcut conv's pre-BN output, normalised in the epilogue
+  // as resid·resid_scale + resid_shift (both or neither)
+  const float* resid_scale;
+  const float* resid_shift;
 };
 bool conv_fwd_bnapply_supported();
 int igemm_tile_m(int cfg);

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void bnfold_wgrad_kernel(const float* __restri
 // statistics slab [2][2][C]: set 0 = 0, set 1 = the value split into fp32 hi + lo (the fp64
 // column reduction restores it); one wave per channel
 __global__ __launch_bounds__(64) void bnfold_rowdot_kernel(const float* __restrict__ G, const uint16_t* __restrict__ w,
-                                                           int C, int K, float* __restrict__ out) {
+                                                           int C, int K, int ns, float* __restrict__ out) {
   const int c = blockIdx.x, lane = threadIdx.x;
   double acc = 0.0;
   for (int k = lane; k < K; k += 64) acc += (double)bf2f(w[(size_t)c * K + k]) * (double)G[(size_t)c * K + k];
@@ -206,18 +206,18 @@ __global__ __launch_bounds__(64) void bnfold_rowdot_kernel(const float* __restri
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if (lane == 0) {
     const float hi = (float)acc, lo = (float)(acc - (double)hi);
-    out[c] = 0.f;
-    out[C + c] = hi;
-    out[2 * C + c] = 0.f;
-    out[3 * C + c] = lo;
+    // two slab rows of ns sets: [0, hi(, 0)] and [0, lo(, 0)] (set 2 = a projection block's
+    // shortcut sums, which its own dgrad epilogue computed)
+    for (int r = 0; r < 2; ++r)
+      for (int j = 0; j < ns; ++j) out[(r * ns + j) * C + c] = j == 1 ? (r == 0 ? hi : lo) : 0.f;
   }
 }
 
 }  // namespace
 
-hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, float* out_rows, hipStream_t s) {
-  if (C <= 0 || K <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bnfold_rowdot_kernel, dim3(C), dim3(64), 0, s, G, (const uint16_t*)w, C, K, out_rows);
+hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, int ns, float* out_rows, hipStream_t s) {
+  if (C <= 0 || K <= 0 || ns < 2 || ns > 3) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_rowdot_kernel, dim3(C), dim3(64), 0, s, G, (const uint16_t*)w, C, K, ns, out_rows);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

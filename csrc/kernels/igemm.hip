@@ -111,9 +111,13 @@ struct IgemmParams {
   int add_pre;   // GemmEpi::add_pre
   int trace;     // g_igemm_trace stamps (diagnostic)
   // FWD VAR 2 (GemmEpi::bn_scale): the block-output BatchNorm applied in the epilogue —
-  // out = relu(bf16(y)·bn_sc + bn_sh + addend), its ReLU bits to mask_out (1 bit per element)
+  // out = relu(bf16(y)·bn_sc + bn_sh + addend), its ReLU bits to mask_out (1 bit per element);
+  // bn_rsc / bn_rsh (projection blocks): the addend is the shortcut's pre-BN output and gets
+  // its own BatchNorm, addend·bn_rsc + bn_rsh (bn_apply residual mode 1)
   const float* bn_sc;
   const float* bn_sh;
+  const float* bn_rsc;
+  const float* bn_rsh;
   uint8_t* mask_out;
   // WGRAD block order: 1 split-major (SDX_WGRAD_ORDER, default), 0 tile-major
   int worder;
@@ -1333,11 +1337,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     bmu_a[q] = bmu_b[q] = bmk_s[q] = bmk_t[q] = 0.f;
     bsum[0][q] = bsum[1][q] = bsum[2][q] = 0.f;
   }
-  float bsc[8], bsh[8];
+  float bsc[8], bsh[8], rsc[8], rsh[8];
+  const bool raff = bnap && p.bn_rsc != nullptr;
   if constexpr (bnap) {
     if (my_col < p.Ncol) {
       load8f(p.bn_sc + my_col, bsc);
       load8f(p.bn_sh + my_col, bsh);
+      if (raff) {
+        load8f(p.bn_rsc + my_col, rsc);
+        load8f(p.bn_rsh + my_col, rsh);
+      }
     }
   }
   if (MODE == MODE_DGRAD && bst && my_col < p.Ncol) {
@@ -1396,8 +1405,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
           unpack8(a_in, rv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) yv[q] = yv[q] * bsc[q] + bsh[q];
+          if (raff) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) yv[q] += rv[q];
+            for (int q = 0; q < 8; ++q) yv[q] += rv[q] * rsc[q] + rsh[q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) yv[q] += rv[q];
+          }
 #pragma unroll
           for (int q = 0; q < 8; ++q) yv[q] = fmaxf(yv[q], 0.f);
           v = pack8(yv);
@@ -1823,6 +1837,8 @@ void set_epi(IgemmParams& p, const GemmEpi* epi) {
   p.add_pre = epi->add_pre;
   p.bn_sc = epi->bn_scale;
   p.bn_sh = epi->bn_shift;
+  p.bn_rsc = epi->resid_scale;
+  p.bn_rsh = epi->resid_shift;
   p.mask_out = epi->mask_out;
   if (epi->resid != nullptr) p.addend = reinterpret_cast<const uint16_t*>(epi->resid);
 }
@@ -1836,8 +1852,8 @@ hipError_t launch_conv_fwd(const ConvGeom& g, const void* x, const void* w, void
   // BN-apply epilogue: stride-1 1x1 geometry (the residual shares the output rows), no
   // statistics / fp32 output / bias; statistics-only pass: y == nullptr needs stats
   if (p.bn_sc != nullptr &&
-      (p.bn_sh == nullptr || p.addend == nullptr || stats != nullptr || p.out_f32 || p.bias != nullptr ||
-       p.relu || in_scale != nullptr || y == nullptr || g.R != 1 || g.S != 1 || g.stride != 1 || g.pad != 0))
+      (p.bn_sh == nullptr || p.addend == nullptr || (p.bn_rsc == nullptr) != (p.bn_rsh == nullptr) ||
+       stats != nullptr || p.out_f32 || p.bias != nullptr || p.relu || in_scale != nullptr || y == nullptr || g.R != 1 || g.S != 1 || g.stride != 1 || g.pad != 0))
     return hipErrorInvalidValue;
   if (y == nullptr && (stats == nullptr || p.bn_sc != nullptr)) return hipErrorInvalidValue;
   p.in_scale = in_scale;

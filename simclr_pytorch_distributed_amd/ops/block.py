@@ -505,14 +505,18 @@ def block_params(mod) -> List[torch.nn.Parameter]:
 
 
 def _fold_fwd(x, info, training, next_native) -> bool:
-    """Forward half of the BN3 fold (block_fwd fold_fwd): identity bottlenecks that fold their
-    BN3 backward AND whose successor is a native block (its final dgrad supplies the slab the
-    folded backward needs, since y3 is not kept)."""
+    """Forward half of the BN3 fold (block_fwd fold_fwd): bottlenecks that fold their BN3
+    backward AND whose successor is a native block (its final dgrad supplies the slab the
+    folded backward needs, since y3 is not kept). Identity blocks add x in conv3's epilogue;
+    projection blocks (any stride) add BN_s(ys), the shortcut BN applied in the same epilogue."""
     convs, bns, bottle, proj = info
-    if not (FOLD_FWD and training and next_native and bottle and not proj and DGRAD_BNSTAT):
+    if not (FOLD_FWD and training and next_native and bottle and DGRAD_BNSTAT):
         return False
-    rows = x.shape[0] * x.shape[1] * x.shape[2]
-    return convs[1].stride == (1, 1) and _fold_eligible(convs, bottle, proj, rows)
+    if not proj and convs[1].stride != (1, 1):
+        return False
+    s = convs[1].stride[0]
+    rows = (x.shape[0] * ((x.shape[1] - 1) // s + 1) * ((x.shape[2] - 1) // s + 1))
+    return _fold_eligible(convs, bottle, proj, rows)
 
 
 def bottleneck(x, blk, wc, training: bool, group=None, chain: Optional[BlockChain] = None,

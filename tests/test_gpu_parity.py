@@ -253,7 +253,8 @@ def test_trajectory_tracks_fp32(gpu):
 def test_bn3_fold_forward_matches(gpu, monkeypatch):
     """Forward half of the BN3 fold (block_fwd fold_fwd: conv3 twice, BN3 + residual + ReLU in
     its epilogue, y3 never stored; backward Σdz·y3 from W3 and dzᵀ·a2) vs the backward-only
-    fold on identity bottleneck pairs of ResNet-50 layers 1-2: the block outputs, their ReLU
+    fold on bottleneck pairs of ResNet-50 layers 1-2, the projection blocks l1.0 (stride 1) and
+    l2.0 (stride 2, shortcut BN applied in conv3's epilogue) included: the block outputs, their ReLU
     bits and the BN running statistics are bit-identical (same conv, same statistics, the
     apply's operations in the same order); every gradient agrees to bf16 noise (Σdz·y3 from
     the unrounded y3)."""
@@ -268,7 +269,7 @@ def test_bn3_fold_forward_matches(gpu, monkeypatch):
     wc = runner.weight_cache()
     nb = list(nat_m.encoder.blocks())
     g = torch.Generator().manual_seed(9)
-    for i in (1, 4, 5):
+    for i in (0, 1, 3, 4, 5):
         hw = 32 if i < 4 else 16
         x = torch.randn(16, hw, hw, nb[i].conv1.in_channels, generator=g).relu().to(gpu).to(torch.bfloat16)
         dy, res = None, {}
