@@ -222,12 +222,44 @@ struct AddPreScope {
   AddPreScope& operator=(const AddPreScope&) = delete;
 };
 
+// K-concatenated BN3-fold dgrad (igemm.hip a2): the next stride-1 1x1 dgrad on this thread
+// reduces over [dy | a2] with wt = [Wd | Mx] ([C][1][1][K + K2]) and adds the fp32 bias
+// before rounding — da2 = dz·Wd + a2·Mx + b in one GEMM instead of a separate T = a2·Mx + b
+// GEMM whose bf16 output the dgrad epilogue re-reads. Scoped like AddPreScope.
+struct FoldCat {
+  const torch::Tensor* a2 = nullptr;
+  const torch::Tensor* bias = nullptr;
+};
+FoldCat& fold_cat() {
+  thread_local FoldCat c;
+  return c;
+}
+struct CatScope {
+  FoldCat saved;
+  CatScope(const torch::Tensor& a2, const torch::Tensor& bias) : saved(fold_cat()) { fold_cat() = {&a2, &bias}; }
+  ~CatScope() { fold_cat() = saved; }
+  CatScope(const CatScope&) = delete;
+  CatScope& operator=(const CatScope&) = delete;
+};
+
 torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                               int64_t cfg, c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> addend,
                               c10::optional<torch::Tensor> addend_mask, BnBwdStat* bs, int64_t addend_sub = 0) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(wt, "wt");
-  TORCH_CHECK(wt.size(3) == dy.size(3), "wt last dim must be Cout");
+  const FoldCat cat = fold_cat();
+  fold_cat() = FoldCat{};   // consumed by this dgrad only
+  const int64_t cat_ch = cat.a2 != nullptr ? cat.a2->size(3) : 0;
+  TORCH_CHECK(wt.size(3) == dy.size(3) + cat_ch, "wt last dim must be Cout (+ the concatenated operand's channels)");
+  if (cat.a2 != nullptr) {
+    check_bf16_nhwc(*cat.a2, "cat a2");
+    TORCH_CHECK(stride == 1 && pad == 0 && wt.size(1) == 1 && wt.size(2) == 1 && !addend.has_value() &&
+                    cat.a2->size(0) == dy.size(0) && cat.a2->size(1) == dy.size(1) && cat.a2->size(2) == dy.size(2),
+                "K-concatenated dgrad: stride-1 1x1, no addend, a2 on dy's pixels");
+    TORCH_CHECK(cat.bias->is_cuda() && cat.bias->scalar_type() == at::kFloat && cat.bias->is_contiguous() &&
+                    cat.bias->numel() == wt.size(0),
+                "K-concatenated dgrad: fp32 bias [C]");
+  }
   ConvGeom g{};
   g.N = dy.size(0); g.P = dy.size(1); g.Q = dy.size(2); g.K = dy.size(3);
   g.C = wt.size(0); g.R = wt.size(1); g.S = wt.size(2);
@@ -237,7 +269,7 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
   TORCH_CHECK(g.C % 8 == 0, "Cin must be a multiple of 8");
   c10::DeviceGuard dg(dy.device());
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true, true);
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * (g.K + cat_ch) / (stride * stride), true, true);
   torch::Tensor dx;
   if (out.has_value()) {
     dx = *out;
@@ -275,6 +307,13 @@ torch::Tensor conv_dgrad_impl(torch::Tensor dy, torch::Tensor wt, int64_t H, int
     // BN3 fold: the addend joins the accumulators before rounding (kernels built with SDX_ADD_PRE)
     static const GemmEpi pre{nullptr, 0, 0, 1};
     const GemmEpi* epi = (fold_add_pre() && add != nullptr && addend_sub == 0 && amask == nullptr) ? &pre : nullptr;
+    GemmEpi ce{};
+    if (cat.a2 != nullptr) {
+      ce.cat_a = cat.a2->data_ptr();
+      ce.cat_ch = (int)cat_ch;
+      ce.bias_pre = cat.bias->data_ptr<float>();
+      epi = &ce;
+    }
     check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), add, (int)cfg,
                                       cur_stream(), amask, bs, add ? (int)addend_sub : 0, epi),
               "conv_dgrad");
@@ -360,7 +399,8 @@ std::vector<torch::Tensor> conv_dgrad_bnstat_impl(torch::Tensor dy, torch::Tenso
   g.C = C; g.R = wt.size(1); g.S = wt.size(2);
   g.H = H; g.W = W; g.stride = stride; g.pad = pad;
   const int64_t M = (int64_t)g.N * g.H * g.W / (stride * stride);
-  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * g.K / (stride * stride), true, true);
+  const int64_t cat_ch = fold_cat().a2 != nullptr ? fold_cat().a2->size(3) : 0;   // (CatScope)
+  if (cfg < 0) cfg = conv_cfg(g, g.K, g.C, M, (int64_t)g.R * g.S * (g.K + cat_ch) / (stride * stride), true, true);
   int rows = 0;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) rows += conv_dgrad_class_mtiles(g, ph, pw, (int)cfg);
@@ -426,7 +466,7 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     return e == nullptr || atoi(e) != 0;
   }();
   const bool w1 = (cfg == 10 || (cfg == -1 && w1_on && splits <= 0)) && !in_scale.has_value() && wgrad1x1_supported(g);
-  TORCH_CHECK(cfg != 10 || w1, "conv_wgrad: cfg 10 needs a 1x1 conv with K,C % 128 == 0 (stride 1, or stride s with H = s*P, W = s*Q)");
+  TORCH_CHECK(cfg != 10 || w1, "conv_wgrad: cfg 10 needs a 1x1 conv with K,C % 128 == 0 (stride 1, or stride s with H = s*P, W = s*Q), or stride 1 with K or C = 64");
   // 64-output-channel GEMMs with a wide reduction side (layer-1 3x3: 64 x 576): the 64x256
   // tile (four 64x64 wave tiles) beats the exact-fit 64x64 one despite its padding, at
   // ~512 blocks (tools/wgrad_split_probe.py: 145 -> 124 us)
@@ -459,7 +499,12 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
         const char* e = getenv("SDX_W3_BLOCKS");
         return e ? atoll(e) : 128LL;
       }();
-      const int64_t target = tail ? tail_blocks : target0;
+      // pixel-pair shapes (HBM-bound, twice the MFMA work per byte): SDX_W1_PAIR_BLOCKS
+      static const int64_t pair_target = [] {
+        const char* e = getenv("SDX_W1_PAIR_BLOCKS");
+        return e ? atoll(e) : 256LL;
+      }();
+      const int64_t target = tail ? tail_blocks : (wgrad1x1_pair_view(g) ? pair_target : target0);
       splits = std::max<int64_t>(1, target / wgrad1x1_tiles(g));
       splits = std::min(splits, std::max<int64_t>(1, steps / 8));
     }
@@ -524,8 +569,9 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
   const float *isc, *ish;
   in_bn_ptrs(in_scale, in_shift, g.C, &isc, &ish);
   torch::Tensor part;
-  if (splits > 1 || accumulate)
-    part = torch::empty({splits * M * Ncol}, x.options().dtype(at::kFloat));
+  const int64_t slices = w1 ? wgrad1x1_slices(g, (int)splits) : splits;
+  if (slices > 1 || accumulate)
+    part = torch::empty({slices * M * Ncol}, x.options().dtype(at::kFloat));
   if (w1) {
     check_hip(launch_wgrad1x1(g, dy.data_ptr(), x.data_ptr(), part.defined() ? part.data_ptr<float>() : nullptr,
                               dw.data_ptr<float>(), (int)splits, accumulate ? 1 : 0, cur_stream()),
@@ -1214,34 +1260,64 @@ void side_fold_wgrad(const torch::Tensor& dz, const torch::Tensor& a2, const tor
   body();
 }
 
-// BN3 fold, main-stream part: Wd = diag(A)·W3 (dgrad layout), then T = a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3
-// (bf16), the D·y3 + E part of dy3 pushed through conv3's data gradient (added by its epilogue)
-std::pair<torch::Tensor, torch::Tensor> fold_dgrad_operands(const torch::Tensor& coef, const torch::Tensor& w3,
-                                                            const torch::Tensor& wt3, const torch::Tensor& a2,
-                                                            const torch::Tensor& mu, const torch::Tensor* gram) {
+// BN3 fold, main-stream part. K-concatenated (SDX_FOLD_CAT, default): one [K][1][1][C + K]
+// bf16 tensor [Wd | Mx] with Wd = diag(A)·W3 (dgrad layout) and Mx = W3ᵀ·diag(D)·W3, plus the
+// fp32 bias b = Eᵀ·W3 — conv3's dgrad then reduces over [dz | a2] (CatScope). Otherwise Wd and
+// T = a2·Mx + b (bf16), the D·y3 + E part of dy3 pushed through conv3's data gradient and
+// added by its epilogue.
+struct FoldOps {
+  torch::Tensor w;      // Wd, or [Wd | Mx] when cat
+  torch::Tensor t;      // T (not cat)
+  torch::Tensor bias;   // b (cat)
+  bool cat = false;
+};
+bool fold_cat_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SDX_FOLD_CAT");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+FoldOps fold_dgrad_operands(const torch::Tensor& coef, const torch::Tensor& w3, const torch::Tensor& wt3,
+                            const torch::Tensor& a2, const torch::Tensor& mu, const torch::Tensor* gram) {
   const int64_t C3 = w3.size(0), K3 = w3.size(3);
   TORCH_CHECK(w3.size(1) == 1 && w3.size(2) == 1 && wt3.size(0) == K3 && wt3.size(3) == C3 && a2.size(3) == K3 &&
                   coef.numel() == 3 * C3,
               "bn3 fold: conv3 must be 1x1 [C][1][1][K] with a2 of K channels");
-  auto wd = torch::empty_like(wt3);
-  auto mx = torch::empty({K3, 1, 1, K3}, w3.options());
-  auto b = torch::empty({K3}, coef.options());
   const int64_t rows = a2.numel() / K3;
-  check_vec(mu, C3, "fold mu");
-  check_hip(launch_bnfold_prep(coef.data_ptr<float>(), w3.data_ptr(), wt3.data_ptr(), (int)C3, (int)K3, wd.data_ptr(),
-                               mx.data_ptr(), b.data_ptr<float>(), mu.data_ptr<float>(),
-                               gram != nullptr ? gram[1].data_ptr<float>() : nullptr, (long)rows, cur_stream()),
-            "bnfold_prep");
   TORCH_CHECK(rows < (1LL << 31), "bn3 fold: too many rows");
+  check_vec(mu, C3, "fold mu");
+  ConvGeom gd{};   // conv3's dgrad: dy = dz (C3 channels) on a2's pixels
+  gd.N = a2.size(0); gd.H = gd.P = a2.size(1); gd.W = gd.Q = a2.size(2);
+  gd.K = (int)C3; gd.C = (int)K3; gd.R = gd.S = 1; gd.stride = 1; gd.pad = 0;
+  FoldOps r;
+  r.bias = torch::empty({K3}, coef.options());
+  const float* cs = gram != nullptr ? gram[1].data_ptr<float>() : nullptr;
+  if (fold_cat_enabled() && conv_dgrad_cat_supported(gd, (int)K3)) {
+    r.cat = true;
+    r.w = torch::empty({K3, 1, 1, C3 + K3}, w3.options());
+    uint16_t* wc = reinterpret_cast<uint16_t*>(r.w.data_ptr());
+    check_hip(launch_bnfold_prep(coef.data_ptr<float>(), w3.data_ptr(), wt3.data_ptr(), (int)C3, (int)K3, wc, wc + C3,
+                                 r.bias.data_ptr<float>(), mu.data_ptr<float>(), cs, (long)rows, cur_stream(),
+                                 (int)(C3 + K3), (int)(C3 + K3)),
+              "bnfold_prep");
+    return r;
+  }
+  r.w = torch::empty_like(wt3);
+  auto mx = torch::empty({K3, 1, 1, K3}, w3.options());
+  check_hip(launch_bnfold_prep(coef.data_ptr<float>(), w3.data_ptr(), wt3.data_ptr(), (int)C3, (int)K3, r.w.data_ptr(),
+                               mx.data_ptr(), r.bias.data_ptr<float>(), mu.data_ptr<float>(), cs, (long)rows,
+                               cur_stream()),
+            "bnfold_prep");
   ConvGeom g{};
   g.N = (int)rows; g.H = g.W = 1; g.C = (int)K3; g.K = (int)K3;
   g.R = g.S = 1; g.P = g.Q = 1; g.stride = 1; g.pad = 0;
-  auto T = torch::empty_like(a2);
-  const GemmEpi epi{b.data_ptr<float>(), 0, 0};
-  check_hip(launch_conv_fwd(g, a2.data_ptr(), mx.data_ptr(), T.data_ptr(), nullptr, auto_cfg(rows, K3, K3, true),
+  r.t = torch::empty_like(a2);
+  const GemmEpi epi{r.bias.data_ptr<float>(), 0, 0};
+  check_hip(launch_conv_fwd(g, a2.data_ptr(), mx.data_ptr(), r.t.data_ptr(), nullptr, auto_cfg(rows, K3, K3, true),
                             cur_stream(), nullptr, nullptr, &epi),
             "bnfold T gemm");
-  return {wd, T};
+  return r;
 }
 
 // bn: [gamma, beta, running_mean, running_var] per BN, in the order bn1, bn2, (bn3), (shortcut bn)
@@ -1524,8 +1600,13 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
       // da2 = dz·(diag(A)·W3) + T: no dy3 tensor; dW3 from dzᵀ·a2 and a2ᵀ·a2 on the side stream
       auto op = fold_dgrad_operands(coef3, fold_w[0], wt[2], a2, S(lastbn, 2), gram3);
       side_fold_wgrad(dz, a2, fold_w[0], coef3, dw[2], side, gram3, Gfold.defined() ? &Gfold : nullptr);
-      AddPreScope pre;
-      r2 = dgrad_bn(dz, op.first, y2, 1, 0, 1, cnt_last, op.second);
+      if (op.cat) {
+        CatScope cs(a2, op.bias);
+        r2 = dgrad_bn(dz, op.w, y2, 1, 0, 1, cnt_last);
+      } else {
+        AddPreScope pre;
+        r2 = dgrad_bn(dz, op.w, y2, 1, 0, 1, cnt_last, op.t);
+      }
     } else {
       side_wgrad(dylast, a2, 1, 1, 1, 0, dw[2], side);
       r2 = dgrad_bn(dylast, wt[2], y2, 1, 0, 1, cnt_last);
@@ -1568,9 +1649,12 @@ std::vector<torch::Tensor> block_bwd(torch::Tensor dout, std::vector<torch::Tens
     // shortcut BN folded like BN3: dx_sc = dz·(diag(A')·Ws) + x·(Wsᵀ·diag(D')·Ws) + E'ᵀ·Ws
     auto op = fold_dgrad_operands(coefs, fold_w[1], wt[nconv], x, S(nconv, 2), grams_sc);
     side_fold_wgrad(dz, x, fold_w[1], coefs, dw[nconv], side, grams_sc);
-    {
+    if (op.cat) {
+      CatScope cs(x, op.bias);
+      dx = conv_dgrad(dz, op.w, H, W, 1, 0, -1, c10::nullopt, c10::nullopt, c10::nullopt, 0);
+    } else {
       AddPreScope pre;
-      dx = conv_dgrad(dz, op.first, H, W, 1, 0, -1, c10::nullopt, op.second, c10::nullopt, 0);
+      dx = conv_dgrad(dz, op.w, H, W, 1, 0, -1, c10::nullopt, op.t, c10::nullopt, 0);
     }
     dx = last_dgrad(dx, dx, c10::nullopt);
   } else if (proj) {
@@ -1632,6 +1716,8 @@ void register_conv_bn(pybind11::module& m) {
         "implicit-GEMM conv forward with a per-channel fp32 bias (+ReLU) epilogue (eval-mode folded BN)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("bias"),
         pybind11::arg("relu"));
+  m.def("wgrad1x1_pairs_set", [](int64_t on) { return (int64_t)wgrad1x1_pairs_set((int)on); },
+        "pixel-pair 1x1 wgrad for 64-channel sides on (1) / off (0); returns the previous value", pybind11::arg("on"));
   m.def("tap3_set", &tap3_set,
         "tap-reuse 3x3 conv loop on (1) / off (0) for auto tile selection; returns the previous value",
         pybind11::arg("on"));
@@ -1653,6 +1739,20 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("pad"), pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),
         pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none(),
         pybind11::arg("addend_sub") = 0);
+  m.def("conv_dgrad_cat",
+        [](torch::Tensor dy, torch::Tensor wt, torch::Tensor a2, torch::Tensor bias, int64_t cfg,
+           c10::optional<torch::Tensor> ya, c10::optional<torch::Tensor> ma) -> std::vector<torch::Tensor> {
+          CatScope cs(a2, bias);
+          if (ya.has_value())
+            return conv_dgrad_bnstat(dy, wt, dy.size(1), dy.size(2), 1, 0, cfg, c10::nullopt, c10::nullopt,
+                                     c10::nullopt, *ya, *ma, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt,
+                                     c10::nullopt);
+          return {conv_dgrad(dy, wt, dy.size(1), dy.size(2), 1, 0, cfg, c10::nullopt, c10::nullopt, c10::nullopt)};
+        },
+        "K-concatenated stride-1 1x1 data gradient dx = dy·Wt[:, :K] + a2·Wt[:, K:] + bias (BN3 fold); with ya / ma "
+        "also the BN-backward statistics slab (ReLU mask recomputed as ya > 0 is not applied: raw sums)",
+        pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("a2"), pybind11::arg("bias"), pybind11::arg("cfg") = -1,
+        pybind11::arg("ya") = pybind11::none(), pybind11::arg("ma") = pybind11::none());
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient (fp32, split-K slab)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("splits") = 0, pybind11::arg("cfg") = -1, pybind11::arg("out") = pybind11::none(),

@@ -41,8 +41,11 @@ hipError_t launch_supcon_bwd(const float* A, const float* C, const int* a_self, 
 // bias = Eᵀ·W3 [K] fp32. wgrad: sink (+)= diag(A)·G + diag(D)·W3·S + E ⊗ cs ([C][K] fp32).
 // mu ([C] mean of y3) / cs ([K] column sums of a2 over `rows`): optional coherent-rounding
 // correction folded into bias (see bnfold.hip)
+// ldw / ldm: row strides of wd / mx in elements (0 = C / K; the K-concatenated fold writes
+// both into one [K][C + K] tensor: wd at column 0, mx at column C)
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
-                              float* bias, const float* mu, const float* cs, long rows, hipStream_t s);
+                              float* bias, const float* mu, const float* cs, long rows, hipStream_t s, int ldw = 0,
+                              int ldm = 0);
 hipError_t launch_bnfold_wgrad(const float* coef, const float* G, const float* S, const float* cs, int ncs,
                                const void* w, int C, int K, float* sink, int accumulate, hipStream_t s);
 // cs[K] = column sums of a [rows][K] bf16 tensor (partial: [bnfold_colsum_blocks()][K] scratch)
@@ -94,7 +97,14 @@ struct GemmEpi {
   // as resid·resid_scale + resid_shift (both or neither)
   const float* resid_scale;
   const float* resid_shift;
+  // DGRAD, stride-1 1x1 only (BN3 fold): K-concatenated second A operand cat_a [pixels][cat_ch]
+  // (reduction over dy's K then cat_a's cat_ch channels; Wt rows of K + cat_ch) and an fp32
+  // per-column bias added before the bf16 rounding
+  const void* cat_a;
+  int cat_ch;
+  const float* bias_pre;
 };
+bool conv_dgrad_cat_supported(const ConvGeom& g, int cat_ch);
 bool conv_fwd_bnapply_supported();
 int igemm_tile_m(int cfg);
 // diagnostic main-loop timeline (SDX_IGEMM_TRACE=1): block 0, waves 0 and 4, s_memtime stamps
@@ -144,11 +154,17 @@ int wgrad3x3_tiles(const ConvGeom& g);
 int wgrad3x3_steps(const ConvGeom& g);
 hipError_t launch_wgrad3x3(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s);
-// Stride-1 1x1 wgrad (wgrad1x1.hip): K % 128 == 0, C % 128 == 0, N*H*W % 32 == 0.
-// partial: fp32 [splits][K][C] (unused when splits == 1 and !accumulate)
+// 1x1 wgrad (wgrad1x1.hip): K % 128 == 0, C % 128 == 0, N*H*W % 32 == 0 (stride 1 or a
+// whole-subgrid strided shortcut), or stride 1 with a 64-channel side (pixel pairs, N*H*W % 64).
+// partial: fp32 [wgrad1x1_slices(g, splits)][K][C] (unused when splits == 1, !accumulate and
+// no pixel pairs)
 bool wgrad1x1_supported(const ConvGeom& g);
 int wgrad1x1_tiles(const ConvGeom& g);
 int wgrad1x1_steps(const ConvGeom& g);
+int wgrad1x1_slices(const ConvGeom& g, int splits);
+bool wgrad1x1_pair_view(const ConvGeom& g);
+// runtime switch of the pixel-pair view (tests / A/B); returns the previous value
+int wgrad1x1_pairs_set(int on);
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s);
 

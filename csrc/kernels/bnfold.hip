@@ -4,7 +4,9 @@
 // W3 [C][K]) the two GEMMs that consumed dy3 are rewritten over dz and a2:
 //
 //   dgrad  da2 = dy3·W3        = dz·(diag(A)·W3) + a2·(W3ᵀ·diag(D)·W3) + Eᵀ·W3
-//                                 └ dgrad, weights Wd ┘ └ T = FWD GEMM, weights Mx, bias b ┘
+//                                 └ weights Wd ┘      └ weights Mx ┘        └ bias b ┘
+//          one K-concatenated GEMM [dz | a2]·[Wd ; Mx] + b (igemm.hip a2 operand, fp32 bias
+//          before the rounding); fallback: a separate T = a2·Mx + b added by the dgrad epilogue
 //   wgrad  dW3 = dy3ᵀ·a2       = diag(A)·G + diag(D)·W3·S + E ⊗ Σa2
 //          with G = dzᵀ·a2 (the wgrad GEMM on dz), S = a2ᵀ·a2, Σa2 the column sums of a2
 //
@@ -33,8 +35,9 @@ constexpr int PREP_NT = 1024;
 __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __restrict__ coef, const uint16_t* __restrict__ w,
                                                           const uint16_t* __restrict__ wt, int C, int K,
                                                           uint16_t* __restrict__ wd, uint16_t* __restrict__ mx,
-                                                          float* __restrict__ bias, const float* __restrict__ mu,
-                                                          const float* __restrict__ cs, float inv_rows) {
+                                                          int ldw, int ldm, float* __restrict__ bias,
+                                                          const float* __restrict__ mu, const float* __restrict__ cs,
+                                                          float inv_rows) {
   extern __shared__ float sm[];   // [C] W[c][l]·D[c], then [PREP_NT] partial sums
   const float* A = coef;
   const float* D = coef + C;
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __res
         float v = acc;
         for (int q = 1; q < P; ++q) v += red[t + q * KW];
         const uint16_t r = f2bf(v);
-        mx[(size_t)l * K + k] = r;
+        mx[(size_t)l * ldm + k] = r;
         if (cs != nullptr) ca = fmaf(cs[k] * inv_rows, v - bf2f(r), ca);
       }
       __syncthreads();
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(PREP_NT) void bnfold_prep_kernel(const float* __res
   const long stride = (long)(gridDim.x - K) * PREP_NT;
   for (long e = (long)(blockIdx.x - K) * PREP_NT + t; e < n; e += stride) {
     const int c = (int)(e % C);
-    wd[e] = f2bf(A[c] * bf2f(wt[e]));
+    wd[(e / C) * ldw + c] = f2bf(A[c] * bf2f(wt[e]));
   }
 }
 
@@ -223,14 +226,18 @@ hipError_t launch_bnfold_rowdot(const float* G, const void* w, int C, int K, int
 }
 
 hipError_t launch_bnfold_prep(const float* coef, const void* w, const void* wt, int C, int K, void* wd, void* mx,
-                              float* bias, const float* mu, const float* cs, long rows, hipStream_t s) {
+                              float* bias, const float* mu, const float* cs, long rows, hipStream_t s, int ldw,
+                              int ldm) {
+  if (ldw == 0) ldw = C;
+  if (ldm == 0) ldm = K;
+  if (ldw < C || ldm < K) return hipErrorInvalidValue;
   if (C <= 0 || K <= 0 || C > 8192 || (K < PREP_NT ? PREP_NT % K : K % PREP_NT) != 0) return hipErrorInvalidValue;
   const long n = (long)K * C;
   int gw = (int)((n + PREP_NT - 1) / PREP_NT);
   if (gw > 256) gw = 256;
   const size_t lds = (size_t)(C + PREP_NT) * sizeof(float);
   hipLaunchKernelGGL(bnfold_prep_kernel, dim3(K + gw), dim3(PREP_NT), lds, s, coef, (const uint16_t*)w,
-                     (const uint16_t*)wt, C, K, (uint16_t*)wd, (uint16_t*)mx, bias, mu, cs,
+                     (const uint16_t*)wt, C, K, (uint16_t*)wd, (uint16_t*)mx, ldw, ldm, bias, mu, cs,
                      rows > 0 ? 1.f / (float)rows : 0.f);
   SDX_LAUNCH_CHECK();
   return hipSuccess;

@@ -101,6 +101,14 @@ struct IgemmParams {
   const uint8_t* addend_mask;
   // operand sizes in elements (bounds checks of the checked build)
   long a_elems, b_elems;
+  // DGRAD, stride-1 1x1 (BN3 fold, K-concatenated): the reduction runs over g.K channels of
+  // dy (rows of g.K) and then a2_ch channels of a2 (rows of a2_ch = g.K >> a2_sh, the same
+  // pixels): [dy | a2]·[Wd ; Mx] in one GEMM. bias_pre: fp32 per-output-column bias added to
+  // the accumulators before the bf16 rounding (the fold's Eᵀ·W3)
+  const uint16_t* a2;
+  int a2_ch, a2_sh;
+  long a2_elems;
+  const float* bias_pre;
   // DGRAD: fused BN-backward statistics of the stored output (BnBwdStat; bs.slab null = off)
   BnBwdStat bs;
   // FWD / DGRAD plain-GEMM epilogue (projection head, csrc/bindings/head_ops.cpp): optional
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
   int b_off[T::B_CH];
   // k decode of this thread's chunk: k = kc + cdim*(ks + ns*kr)
   int kc = 0, ks = 0, kr = 0;
-  const int cdim = (MODE == MODE_FWD) ? g.C : g.K;
+  const int cdim = (MODE == MODE_FWD) ? g.C : g.K + p.a2_ch;
   const int tap_s = (MODE == MODE_DGRAD) ? p.ns : g.S;
   if (MODE != MODE_WGRAD) {
     const int hw_out = (MODE == MODE_FWD) ? g.P * g.Q : p.Hc * p.Wc;
@@ -693,12 +701,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
       const int tap = u_kr * tap_s + u_ks;
       const int toff = (MODE == MODE_FWD) ? (u_kr * g.W + u_ks) * g.C + u_c0 : -(u_kr * g.Q + u_ks) * g.K + u_c0;
       const int lane_c = kin_ch * 8;
+      // K-concatenated second operand (wave-uniform: g.K % BK == 0)
+      const bool cat2 = MODE == MODE_DGRAD && u_c0 >= g.K;
 #pragma unroll
       for (int i = 0; i < FCH; ++i) {
         const bool ok = kok && ((vmask[i] >> tap) & 1u);
-        const int off = rbase[i] + toff + lane_c;
-        SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
-        const gptr16 src = ok ? (gptr16)(p.a + off) : zp;
+        const int off = cat2 ? (rbase[i] >> p.a2_sh) + (u_c0 - g.K) + lane_c : rbase[i] + toff + lane_c;
+        SDX_DCHECK(!ok || (off >= 0 && off + 8 <= (cat2 ? p.a2_elems : p.a_elems)));
+        const gptr16 src = ok ? (gptr16)((cat2 ? p.a2 : p.a) + off) : zp;
         glds16(src, sa + 8 * (wvu * T::A_CH + i) * BK * 2);
       }
       const int kb = p.b_t0 + u_kr * p.b_tr + u_ks * p.b_ts + u_c0 + lane_c;
@@ -728,6 +738,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     // one multiply per K-tile, then per row a bounds test and an add (no 1x1 special case:
     // its taps stay (0, 0))
     const int toff = (MODE == MODE_FWD) ? (kr * g.W + ks) * g.C + kc : kc - (kr * g.Q + ks) * g.K;
+    // K-concatenated second operand (1x1: kr = ks = 0; the side is uniform per K-tile)
+    const bool cat2 = MODE == MODE_DGRAD && kc >= g.K;
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
       bool ok;
@@ -735,9 +747,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
         ok = kok && (unsigned)(a_y[i] + kr) < (unsigned)g.H && (unsigned)(a_x[i] + ks) < (unsigned)g.W;
       else
         ok = kok && (unsigned)(a_y[i] - kr) < (unsigned)g.P && (unsigned)(a_x[i] - ks) < (unsigned)g.Q;
-      const int off = a_rb[i] + toff;
-      SDX_DCHECK(!ok || (off >= 0 && off + 8 <= p.a_elems));
-      const gptr16 src = ok ? (gptr16)(p.a + off) : zp;
+      const int off = cat2 ? (a_rb[i] >> p.a2_sh) + (kc - g.K) : a_rb[i] + toff;
+      SDX_DCHECK(!ok || (off >= 0 && off + 8 <= (cat2 ? p.a2_elems : p.a_elems)));
+      const gptr16 src = ok ? (gptr16)((cat2 ? p.a2 : p.a) + off) : zp;
       glds16(src, sa + 8 * (wvu * T::A_CH + i) * BK * 2);
     }
     const int kb = p.b_t0 + kr * p.b_tr + ks * p.b_ts + kc;
@@ -1214,6 +1226,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     return;
   }
 
+  if (MODE == MODE_DGRAD && p.bias_pre != nullptr) {
+    // per-column fp32 bias joins the accumulators before the single bf16 rounding
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WTN + 16 * j + 4 * h;
+      if (col < p.Ncol) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bias_pre + col);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          acc[i][j][0] += b.x;
+          acc[i][j][1] += b.y;
+          acc[i][j][2] += b.z;
+          acc[i][j][3] += b.w;
+        }
+      }
+    }
+  }
 #if SDX_ADD_PRE
   if (MODE == MODE_DGRAD && p.add_pre && p.addend != nullptr) {
     // the addend joins the fp32 accumulators, so the sum is rounded to bf16 once (a small
@@ -1710,7 +1739,7 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
     // 8-wave 256x128 / 128x256 tiles at more than two K-tiles whose channel dim (FWD C,
     // DGRAD K) is a multiple of BK (branch-free K decode): the in-wave pipelined loop (DEPTH 6)
     constexpr bool kW1 = WM * WN == 8 && BM * BN == 256 * 128;
-    const int cdim_h = MODE == MODE_FWD ? p.g.C : p.g.K;
+    const int cdim_h = MODE == MODE_FWD ? p.g.C : p.g.K + p.a2_ch;
     const int taps_h = MODE == MODE_FWD ? p.g.R * p.g.S : p.nr * p.ns;
     const bool w1 = kW1 && p.Kdim > 2 * BK && p.in_scale == nullptr && cdim_h % BK == 0 && taps_h <= 32;
     if (p.in_scale == nullptr && igemm_glds() != 0) {
@@ -1720,6 +1749,7 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
       return launch_k<MODE, BM, BN, WM, WN, 3>(bs, grid, p, s);
     }
   }
+  if (p.a2 != nullptr) return hipErrorInvalidValue;   // K-concatenation: LDS-DMA loops only
   if constexpr (kDepth2) {
     if (igemm_depth() == 2 && !bs) {
       hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, 2, 0, false>), dim3(grid), dim3(64 * WM * WN), 0, s, p);
@@ -1838,6 +1868,9 @@ void set_epi(IgemmParams& p, const GemmEpi* epi) {
   p.bn_sc = epi->bn_scale;
   p.bn_sh = epi->bn_shift;
   p.bn_rsc = epi->resid_scale;
+  p.a2 = reinterpret_cast<const uint16_t*>(epi->cat_a);
+  p.a2_ch = epi->cat_ch;
+  p.bias_pre = epi->bias_pre;
   p.bn_rsh = epi->resid_shift;
   p.mask_out = epi->mask_out;
   if (epi->resid != nullptr) p.addend = reinterpret_cast<const uint16_t*>(epi->resid);
@@ -1892,6 +1925,15 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
   return (M + bm - 1) / bm;
 }
 
+// K-concatenated dgrad [dy | a2]·[Wd ; Mx] (BN3 fold): a stride-1 unpadded 1x1 whose dy
+// width is a power-of-two multiple of a2's (both multiples of BK), on the LDS-DMA loops
+bool conv_dgrad_cat_supported(const ConvGeom& g, int cat_ch) {
+  if (cat_ch <= 0 || g.R != 1 || g.S != 1 || g.stride != 1 || g.pad != 0 || g.P != g.H || g.Q != g.W) return false;
+  if (g.K % BK != 0 || cat_ch % BK != 0 || g.K % cat_ch != 0) return false;
+  const unsigned r = (unsigned)(g.K / cat_ch);
+  return (r & (r - 1)) == 0 && igemm_glds() != 0;
+}
+
 hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void* dy, const void* wt, void* dx,
                                    const void* addend, int cfg, hipStream_t s, const void* addend_mask,
                                    const BnBwdStat* bstat, int addend_sub, const GemmEpi* epi) {
@@ -1915,6 +1957,15 @@ hipError_t launch_conv_dgrad_class(const ConvGeom& g, int ph, int pw, const void
   p.Ncol = g.C;
   p.Kdim = p.nr * p.ns * g.K;
   p.b_row = g.R * g.S * g.K;
+  if (p.a2 != nullptr || p.a2_ch != 0) {
+    if (p.a2 == nullptr || !conv_dgrad_cat_supported(g, p.a2_ch)) return hipErrorInvalidValue;
+    p.a2_sh = __builtin_ctz((unsigned)(g.K / p.a2_ch));
+    p.a2_elems = (long)g.N * g.P * g.Q * p.a2_ch;
+    p.Kdim += p.a2_ch;
+    p.b_row += p.a2_ch;
+  }
+  if (p.bias_pre != nullptr && (g.stride != 1 || (reinterpret_cast<uintptr_t>(p.bias_pre) & 15) != 0))
+    return hipErrorInvalidValue;
   p.b_t0 = (p.r0 * g.S + p.s0) * g.K;
   p.b_tr = g.stride * g.S * g.K;
   p.b_ts = g.stride * g.K;

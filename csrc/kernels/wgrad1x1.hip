@@ -20,7 +20,8 @@
 // networks/resnet_big.py:44-49, conv1/conv3 of each Bottleneck), and the strided projection
 // shortcuts (:50-55) on the pipelined kernel (an x chunk reads its pixel at base + step·const
 // when a step is whole output rows, else from g / Q per step). The layer-1 1x1 wgrads (64
-// channels on one side) are HBM-bound and stay on the generic kernel.
+// channels on one side, HBM-bound) run on the same kernel over a pixel-pair view (w1_pairs).
+#include <atomic>
 #include <type_traits>
 
 #include "common.h"
@@ -75,6 +76,10 @@ struct W1Params {
   unsigned xmagic;
   int steps_per_split;
   int k_tiles, c_tiles, splits;
+  // pixel pairs (a 64-channel side, stride 1): K, C above are the doubled widths of the
+  // [pixels / 2][2·K0] / [pixels / 2][2·C0] views; only the diagonal blocks (even pixel x even
+  // pixel, odd x odd) are stored, into slices 2·split and 2·split + 1 of a [2·splits][K0][C0] slab
+  int pairs, K0, C0;
 };
 
 template <int BN>
@@ -217,6 +222,25 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_kernel(W1Params p) {
   }
 
   // ---- epilogue: fp32 partial rows, 4 consecutive columns per lane ----
+  if (p.pairs) {
+    // the diagonal blocks only: row m of dy half e = m / K0, column n of x half n / C0 (4
+    // consecutive columns never straddle C0, a multiple of 64)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = k0 + wm * 64 + 16 * i + c16;
+      const int e = m >= p.K0;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = c0 + wn * WN_COLS + 16 * j + 4 * h4;
+        if ((n >= p.C0) != e) continue;
+        const f32x4 a = acc[i][j];
+        float* o = p.part + ((size_t)(2 * split + e) * p.K0 + (m - e * p.K0)) * p.C0 + (n - e * p.C0);
+        st16<SDX_NT_PART != 0>(o, make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                             __float_as_uint(a[3])));
+      }
+    }
+    return;
+  }
   float* out = p.part + (size_t)split * p.K * p.C;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -423,6 +447,25 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
     iter(b0, I3{});
   }
 
+  if (p.pairs) {
+    // the diagonal blocks only: row m of dy half e = m / K0, column n of x half n / C0 (4
+    // consecutive columns never straddle C0, a multiple of 64)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = k0 + wm * 64 + 16 * i + c16;
+      const int e = m >= p.K0;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = c0 + wn * WN_COLS + 16 * j + 4 * h4;
+        if ((n >= p.C0) != e) continue;
+        const f32x4 a = acc[i][j];
+        float* o = p.part + ((size_t)(2 * split + e) * p.K0 + (m - e * p.K0)) * p.C0 + (n - e * p.C0);
+        st16<SDX_NT_PART != 0>(o, make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                             __float_as_uint(a[3])));
+      }
+    }
+    return;
+  }
   float* out = p.part + (size_t)split * p.K * p.C;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -440,13 +483,37 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
 
 // SDX_W1_BN=128 forces the 128-column tile on every shape (co-residency experiments: the
 // non-pipelined 128x128 kernel holds 112 VGPRs, so an 8-wave main-stream block fits beside it)
+// pixel-pair view (stride 1, a 64-channel side: the layer-1 bottleneck 1x1 convs, reference
+// networks/resnet_big.py:44,48 at planes = 64): two consecutive pixels' 64 channels form one
+// 128-wide row, so the kernel's 128-row / 128-column tiles stay whole. The GEMM over the
+// pair view also forms the even x odd cross blocks (MFMA work thrown away: these GEMMs are
+// HBM-bound), while dy and x are read at full 16-B chunks in one pass
+//
+// Opt-in (SDX_W1_PAIRS=1, or wgrad1x1_pairs_set): measured no faster than the generic
+// kernel at CIFAR (65-68 vs 70 us stand-alone at 256 blocks, in-step within noise) and slower
+// at config 5 (71.3 vs 70.5 ms/step): the 32-pixel-pair step loop is latency-bound once its
+// MFMA work doubles (profiles/wgrad1x1_pairs_r5.txt)
+std::atomic<int>& w1_pairs_flag() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("SDX_W1_PAIRS");
+    return e != nullptr && atoi(e) != 0 ? 1 : 0;
+  }()};
+  return on;
+}
+bool w1_pairs(const ConvGeom& g) {
+  return w1_pairs_flag().load(std::memory_order_relaxed) != 0 && g.stride == 1 && g.R == 1 && g.S == 1 && g.pad == 0 && (g.K == 64 || g.C == 64) && g.K % 64 == 0 &&
+         g.C % 64 == 0 && ((long)g.N * g.P * g.Q) % 64 == 0;
+}
+int w1_kv(const ConvGeom& g) { return w1_pairs(g) ? 2 * g.K : g.K; }
+int w1_cv(const ConvGeom& g) { return w1_pairs(g) ? 2 * g.C : g.C; }
+
 int wgrad1x1_bn(const ConvGeom& g) {
   static const int force = [] {
     const char* e = getenv("SDX_W1_BN");
     return e ? atoi(e) : 0;
   }();
   if (force == 128) return 128;
-  return g.C % 256 == 0 ? 256 : 128;
+  return w1_cv(g) % 256 == 0 ? 256 : 128;
 }
 
 bool w1_pipe_enabled(const ConvGeom& g) {
@@ -472,13 +539,21 @@ bool wgrad1x1_supported(const ConvGeom& g) {
   const bool strided_ok = strided_on && g.stride > 1 && g.H == g.stride * g.P && g.W == g.stride * g.Q &&
                           (long)g.N * g.P * g.Q * g.Q < (1L << 32) &&
                           w1_pipe_enabled(g);
+  if (g.R == 1 && g.S == 1 && g.pad == 0 && g.stride == 1 && g.P == g.H && g.Q == g.W && w1_pairs(g))
+    return w1_pipe_enabled(g);
   return g.R == 1 && g.S == 1 && g.pad == 0 && (g.stride == 1 ? (g.P == g.H && g.Q == g.W) : strided_ok) &&
          g.K % W1_BM == 0 && g.C % 128 == 0 && ((long)g.N * g.P * g.Q) % 32 == 0;
 }
 
-int wgrad1x1_tiles(const ConvGeom& g) { return (g.K / W1_BM) * (g.C / wgrad1x1_bn(g)); }
+int wgrad1x1_tiles(const ConvGeom& g) { return (w1_kv(g) / W1_BM) * (w1_cv(g) / wgrad1x1_bn(g)); }
 
-int wgrad1x1_steps(const ConvGeom& g) { return (int)((long)g.N * g.P * g.Q / 32); }
+int wgrad1x1_steps(const ConvGeom& g) { return (int)((long)g.N * g.P * g.Q / (w1_pairs(g) ? 64 : 32)); }
+
+int wgrad1x1_slices(const ConvGeom& g, int splits) { return w1_pairs(g) ? 2 * splits : splits; }
+
+bool wgrad1x1_pair_view(const ConvGeom& g) { return w1_pairs(g); }
+
+int wgrad1x1_pairs_set(int on) { return w1_pairs_flag().exchange(on ? 1 : 0); }
 
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s) {
@@ -486,12 +561,15 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   W1Params p{};
   p.dy = (const uint16_t*)dy;
   p.x = (const uint16_t*)x;
-  p.K = g.K;
-  p.C = g.C;
+  p.pairs = w1_pairs(g) ? 1 : 0;
+  p.K0 = g.K;
+  p.C0 = g.C;
+  p.K = w1_kv(g);
+  p.C = w1_cv(g);
   p.steps_total = wgrad1x1_steps(g);
   if (g.stride == 1) {
     p.xst = 1, p.xq = 32, p.xw = 32;   // xpix(j) = j
-    p.x_step = 32 * g.C;
+    p.x_step = 32 * p.C;
   } else {
     p.xst = g.stride, p.xq = g.Q, p.xw = g.W;
     p.x_step = 32 % g.Q == 0 ? g.stride * g.W * (32 / g.Q) * g.C : 0;
@@ -500,9 +578,9 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   p.steps_per_split = (p.steps_total + splits - 1) / splits;
   p.splits = (p.steps_total + p.steps_per_split - 1) / p.steps_per_split;
   const int bn = wgrad1x1_bn(g);
-  p.k_tiles = g.K / W1_BM;
-  p.c_tiles = g.C / bn;
-  const bool direct = p.splits == 1 && !accumulate;
+  p.k_tiles = p.K / W1_BM;
+  p.c_tiles = p.C / bn;
+  const bool direct = p.splits == 1 && !accumulate && !p.pairs;
   if (!direct && partial == nullptr) return hipErrorInvalidValue;
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W1_NT);
@@ -523,5 +601,5 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   }
   SDX_LAUNCH_CHECK();
   if (direct) return hipSuccess;
-  return launch_splitk_reduce(partial, p.splits, (long)g.K * g.C / 4, dw, accumulate, s);
+  return launch_splitk_reduce(partial, p.pairs ? 2 * p.splits : p.splits, (long)g.K * g.C / 4, dw, accumulate, s);
 }

@@ -110,13 +110,15 @@ def test_wgrad3x3_tap_reuse(gpu, shape, splits):
 
 
 @pytest.mark.parametrize("shape", [(4, 16, 256, 128), (2, 8, 512, 256), (8, 4, 128, 512), (3, 8, 384, 128),
-                                   (6, 4, 256, 128), (16, 16, 256, 256)])
+                                   (6, 4, 256, 128), (16, 16, 256, 256),
+                                   (4, 16, 64, 256), (4, 16, 256, 64), (2, 16, 64, 64), (3, 8, 64, 128),
+                                   (3, 8, 128, 64)])
 @pytest.mark.parametrize("splits", [1, 3, 0])
 def test_wgrad1x1_stream(gpu, shape, splits):
     """Stride-1 1x1 wgrad kernels (cfg 10, wgrad1x1.hip) vs fp32 torch: 128- and 256-wide
     column tiles, direct / split-K / auto split, accumulation into a sink, auto dispatch.
-    Pixel counts that are multiples of 64 run the LDS-DMA kernel, (6, 4, ...) = 96 pixels
-    the register-staged one."""
+    A 64-channel side (the last five shapes) runs on the opt-in pixel-pair view: two pixels'
+    64 channels per 128-wide row, the diagonal blocks stored as two slab slices per split."""
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
     N, H, C, K = shape
@@ -126,6 +128,14 @@ def test_wgrad1x1_stream(gpu, shape, splits):
     dy = torch.randn_like(out).bfloat16()
     (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
     dyh, xh = dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    prev = m.wgrad1x1_pairs_set(1)   # the pixel-pair view is opt-in
+    try:
+        _wgrad1x1_checks(m, dyh, xh, dw_ref, splits, K, C, gpu)
+    finally:
+        m.wgrad1x1_pairs_set(prev)
+
+
+def _wgrad1x1_checks(m, dyh, xh, dw_ref, splits, K, C, gpu):
     dw = m.conv_wgrad(dyh, xh, 1, 1, 1, 0, splits, 10)
     assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
     sink = torch.full((K, 1, 1, C), 0.25, device=gpu)
@@ -407,3 +417,33 @@ def test_dgrad_compact_subgrid_addend(gpu, shape):
     r_ref = m.conv_dgrad_bnstat(dy1, wt1, H, W, 1, 0, -1, None, full, None, y, mu)
     r = m.conv_dgrad_bnstat(dy1, wt1, H, W, 1, 0, -1, None, compact, None, y, mu, addend_sub=2)
     assert torch.equal(r[0], r_ref[0]) and torch.allclose(r[1], r_ref[1], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 256, 64), (2, 8, 512, 128), (2, 8, 1024, 256), (3, 8, 256, 128)])
+@pytest.mark.parametrize("cfg", [-1, 1, 4, 6])
+def test_conv_dgrad_cat(gpu, shape, cfg):
+    """K-concatenated stride-1 1x1 dgrad (BN3 fold: da2 = dz·Wd + a2·Mx + b in one GEMM,
+    igemm.hip a2 operand) vs fp32 torch, on the DEPTH 3 (cfgs 1, 4) and DEPTH 6 (cfg 6)
+    LDS-DMA loops; with the BN-statistics epilogue the same dx and the slab's sums."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, K, K2 = shape
+    C = K2
+    g = torch.Generator(device="cpu").manual_seed(3)
+    dy = torch.randn(N, H, H, K, generator=g).bfloat16().to(gpu)
+    a2 = torch.randn(N, H, H, K2, generator=g).bfloat16().to(gpu)
+    wcat = (torch.randn(C, 1, 1, K + K2, generator=g) / (K + K2) ** 0.5).bfloat16().to(gpu)
+    bias = torch.randn(C, generator=g).to(gpu)
+    wf = wcat.float().reshape(C, K + K2)
+    ref = dy.float().reshape(-1, K) @ wf[:, :K].t() + a2.float().reshape(-1, K2) @ wf[:, K:].t() + bias
+    dx = m.conv_dgrad_cat(dy, wcat, a2, bias, cfg)[0]
+    assert dx.shape == (N, H, H, C)
+    assert _rel(dx.reshape(-1, C), ref) < 1e-2
+    ya = torch.randn(N, H, H, C, generator=g).bfloat16().to(gpu)
+    ma = torch.randn(C, generator=g).to(gpu)
+    dx2, slab = m.conv_dgrad_cat(dy, wcat, a2, bias, cfg, ya, ma)
+    assert torch.equal(dx2, dx)
+    s = slab.double().sum(0)
+    d = dx.double().reshape(-1, C)
+    assert torch.allclose(s[0], d.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s[1], (d * (ya.double().reshape(-1, C) - ma.double())).sum(0), rtol=1e-4, atol=1e-1)
