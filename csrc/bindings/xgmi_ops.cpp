@@ -24,6 +24,7 @@ struct Arena {
   std::vector<void*> opened;       // peer arenas mapped through IPC
   XgmiPeers peers{};
   unsigned epoch = 0;
+  unsigned* epoch_dev = nullptr;   // device [epoch, ticket] per (virtual) rank (XgmiCol::epoch_ctr)
   int* err = nullptr;              // host-pinned, GPU-written error word (sender index + 1)
   long long timeout_ticks = 0;     // flag-poll deadline in 100 MHz wall-clock ticks
   double ticks_per_s = 1e8;        // wall-clock rate
@@ -69,6 +70,8 @@ int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, double timeout_s) 
   // uncached: peers' remote stores must be seen by this GPU's loads without cache maintenance
   check_hip(hipExtMallocWithFlags(&a->base, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
   check_hip(hipMemset(a->base, 0, bytes), "hipMemset");
+  check_hip(hipMalloc(reinterpret_cast<void**>(&a->epoch_dev), 2 * sizeof(unsigned)), "hipMalloc(epochs)");
+  check_hip(hipMemset(a->epoch_dev, 0, 2 * sizeof(unsigned)), "hipMemset(epochs)");
   a->peers.cap = a->cap;
   set_ptrs(a->peers, a->rank, a->base, a->world, a->cap);
   // error word in coherent host memory: the kernel stores it (system scope) and the host
@@ -119,7 +122,7 @@ torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x, double timeout_s) {
   auto out = torch::empty_like(x);
   a.epoch += 1;
   check_hip(launch_xgmi_allreduce(x.data_ptr<double>(), out.data_ptr<double>(), (int)x.numel(), a.peers, a.rank,
-                                  a.world, a.epoch, a.err, call_ticks(a, timeout_s), cur_stream()),
+                                  a.world, a.epoch, a.err, call_ticks(a, timeout_s), cur_stream(), a.epoch_dev),
             "xgmi_allreduce");
   return out;
 }
@@ -139,6 +142,7 @@ void xgmi_destroy(int64_t id) {
   (void)hipDeviceSynchronize();
   for (void* p : a->opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(a->base);
+  (void)hipFree(a->epoch_dev);
   (void)hipHostFree(a->err);
 }
 
@@ -165,6 +169,9 @@ int64_t xgmi_emu_create(int64_t world, int64_t cap, double timeout_s) {
   const size_t one = arena_bytes(a->world, a->cap);
   check_hip(hipMalloc(&a->base, one * world), "hipMalloc(emulated arenas)");
   check_hip(hipMemset(a->base, 0, one * world), "hipMemset");
+  check_hip(hipMalloc(reinterpret_cast<void**>(&a->epoch_dev), (size_t)world * 2 * sizeof(unsigned)),
+            "hipMalloc(epochs)");
+  check_hip(hipMemset(a->epoch_dev, 0, (size_t)world * 2 * sizeof(unsigned)), "hipMemset(epochs)");
   a->peers.cap = a->cap;
   for (int q = 0; q < a->world; ++q) set_ptrs(a->peers, q, static_cast<char*>(a->base) + one * q, a->world, a->cap);
   check_hip(hipHostMalloc(reinterpret_cast<void**>(&a->err), sizeof(int), hipHostMallocCoherent | hipHostMallocMapped),
@@ -220,6 +227,8 @@ XgmiCol xgmi_col_args(int64_t id) {
   x.me = a.rank;
   x.world = a.world;
   x.epoch = ++a.epoch;
+  // real peers: this rank's counter row; emulated: one row per virtual rank (z)
+  x.epoch_ctr = a.epoch_dev;
   x.err = a.err;
   x.timeout_ticks = a.timeout_ticks;
   x.slab_zstride = 0;

@@ -215,6 +215,13 @@ struct XgmiCol {
   XgmiPeers peers;
   int mode = 0, me = 0, world = 1;
   unsigned epoch = 0;
+  // device-side epoch (null: the host `epoch`): per rank (emulated: per virtual rank) a pair
+  // [epoch, groups-done ticket]. Every column group's last block takes epoch + 1 for this
+  // exchange; the last group to finish stores it back. One epoch sequence per rank for every
+  // exchange and one-shot call on the arena, so parities alternate launch by launch, and a
+  // launch replayed from a hipGraph advances its own epoch (a host argument would be frozen
+  // at capture and the flag waits would pass on stale flags)
+  unsigned* epoch_ctr = nullptr;
   int* err = nullptr;               // host-pinned: 1 + sender whose flag missed the deadline
   long long timeout_ticks = 0;      // 100 MHz wall-clock ticks
   long slab_zstride = 0;            // mode 2: elements between virtual ranks' slabs
@@ -292,8 +299,10 @@ hipError_t launch_unpad_add(const float* src, float* dst, int rows, int Cp, int 
 // ---- one-shot small all-reduce over xGMI peer memory (xgmi.hip) --------------------
 // err: host-pinned int (1 + rank of a peer whose flag missed the deadline of timeout_ticks
 // of the 100 MHz wall clock; the sum is then skipped)
+// epoch_ctr (optional): the arena's device epoch pair (XgmiCol::epoch_ctr); `epoch` then unused
 hipError_t launch_xgmi_allreduce(const double* in, double* out, int n, const XgmiPeers& peers, int me, int world,
-                                 unsigned epoch, int* err, long long timeout_ticks, hipStream_t s);
+                                 unsigned epoch, int* err, long long timeout_ticks, hipStream_t s,
+                                 unsigned* epoch_ctr = nullptr);
 // bounded single-wave sleep on stream s (watchdog tests)
 hipError_t launch_gpu_stall(long long ticks, hipStream_t s);
 hipError_t launch_xgmi_emulate(const double* in, double* out, int n, const XgmiPeers& peers, int world,

@@ -57,7 +57,16 @@ template <int NS, int XG>
 __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, int me) {
   constexpr int kScope = XG == 1 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   const int W = xg.world;
-  const int par = xg.epoch & 1;
+  // this exchange's epoch: the rank's device epoch + 1 (graph-replay safe), else the host's.
+  // Pair [epoch, ticket] per rank (per virtual rank when emulated); the group finishing last
+  // stores the new epoch, after every group of this launch has read the old one
+  unsigned* ctr = xg.epoch_ctr != nullptr ? xg.epoch_ctr + 2 * (XG == 2 ? me : 0) : nullptr;
+  __shared__ unsigned ep_s;
+  if (threadIdx.x == 0)
+    ep_s = ctr != nullptr ? __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : xg.epoch;
+  __syncthreads();
+  const unsigned epoch = ep_s;
+  const int par = epoch & 1;
   const size_t cap = xg.peers.cap;
   __shared__ int ok;
   if (threadIdx.x < 64 && c < C) {
@@ -78,7 +87,7 @@ __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, in
     // this rank's flag to peer p; solo mode (one rank's share, diagnostic) then polls only
     // its own slot (the other W-1 ranks count as already published)
     const int p = threadIdx.x;
-    __hip_atomic_store(xg.peers.flags[p] + ((size_t)par * W + me) * kXgmiFlagGroups + blockIdx.x, xg.epoch,
+    __hip_atomic_store(xg.peers.flags[p] + ((size_t)par * W + me) * kXgmiFlagGroups + blockIdx.x, epoch,
                        __ATOMIC_RELAXED, kScope);
   }
   if (threadIdx.x < W && !(XG == 2 && xg.solo && threadIdx.x != me)) {
@@ -86,7 +95,7 @@ __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, in
     unsigned* f = xg.peers.flags[me] + ((size_t)par * W + p) * kXgmiFlagGroups + blockIdx.x;
     const long long t0 = wall_clock64();
     unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, kScope) != xg.epoch) {
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, kScope) != epoch) {
       if ((++spins & 63) == 0 && wall_clock64() - t0 > xg.timeout_ticks) {
         atomicExch(&ok, 0);
         if (xg.err) __hip_atomic_store(xg.err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -96,6 +105,13 @@ __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, in
     }
   }
   __syncthreads();
+  if (ctr != nullptr && threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {   // every column group of this launch has taken its epoch
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (!ok) return false;
   if (threadIdx.x < 64 && c < C) {
     const unsigned long long* base =

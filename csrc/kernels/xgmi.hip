@@ -36,7 +36,14 @@ namespace {
 
 template <int SCOPE>
 __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__ out, int n, const XgmiPeers& peers,
-                             int me, int world, unsigned epoch, int* err, long long timeout_ticks) {
+                             int me, int world, unsigned epoch_host, int* err, long long timeout_ticks,
+                             unsigned* ctr = nullptr) {
+  // the arena's device epoch (XgmiCol::epoch_ctr: [epoch, ticket]) when given, else the host's
+  __shared__ unsigned ep_s;
+  if (threadIdx.x == 0)
+    ep_s = ctr != nullptr ? __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : epoch_host;
+  __syncthreads();
+  const unsigned epoch = ep_s;
   const int par = epoch & 1;
   const size_t cap = peers.cap;
   // 1. scatter my contribution into every arena
@@ -78,6 +85,7 @@ __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__
     }
   }
   __syncthreads();
+  if (ctr != nullptr && threadIdx.x == 0) __hip_atomic_store(ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!ok_all) return;
   if (SCOPE == 1)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -94,8 +102,9 @@ __device__ void oneshot_body(const double* __restrict__ in, double* __restrict__
 }
 
 __global__ __launch_bounds__(256) void oneshot_kernel(const double* in, double* out, int n, XgmiPeers peers, int me,
-                                                      int world, unsigned epoch, int* err, long long timeout_ticks) {
-  oneshot_body<1>(in, out, n, peers, me, world, epoch, err, timeout_ticks);
+                                                      int world, unsigned epoch, int* err, long long timeout_ticks,
+                                                      unsigned* ctr) {
+  oneshot_body<1>(in, out, n, peers, me, world, epoch, err, timeout_ticks, ctr);
 }
 
 // block b = virtual rank b; in/out are [W][n]; peers.data/flags are the W local arenas
@@ -117,11 +126,11 @@ __global__ __launch_bounds__(64) void stall_kernel(long long ticks) {
 }  // namespace
 
 hipError_t launch_xgmi_allreduce(const double* in, double* out, int n, const XgmiPeers& peers, int me, int world,
-                                 unsigned epoch, int* err, long long timeout_ticks, hipStream_t s) {
+                                 unsigned epoch, int* err, long long timeout_ticks, hipStream_t s, unsigned* epoch_ctr) {
   if (n < 0 || (size_t)n > peers.cap || world < 1 || world > kXgmiMaxPeers || timeout_ticks <= 0)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(oneshot_kernel, dim3(1), dim3(256), 0, s, in, out, n, peers, me, world, epoch, err,
-                     timeout_ticks);
+                     timeout_ticks, epoch_ctr);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -499,17 +499,14 @@ class PretrainEngine:
     def enable_cuda_graph(self, idx_example: torch.Tensor, warmup: int = 2) -> bool:
         """Capture the whole training step (aug → fwd → loss → bwd → SGD) in one hipGraph.
 
-        Single-process only (the data-parallel path keeps eager launches). Capture needs
+        Single-process only (the data-parallel path keeps eager launches; an emulated SyncBN
+        group — SDX_SYNCBN_EMU — is captured too: the fused exchange takes its epoch from
+        device-side counters, so every replay advances it, bn.hip xg_exchange). Capture needs
         warm-up steps run on a side stream; they execute real updates, so the training
         state they touch (parameters, optimizer buffers, BN running statistics, the norm
         EMA) is snapshotted first and restored after the capture — a graphed run follows
         exactly the eager trajectory."""
         if self.device.type != "cuda" or self.world > 1 or self.backend != "native":
-            return False
-        # the fused SyncBN exchange takes its epoch as a host-side kernel argument: a captured
-        # launch would replay a stale epoch and pass its flag waits at once (ADVICE r3), so an
-        # emulated (or any native xGMI) SyncBN group keeps eager launches
-        if isinstance(self.sync_group, comm.EmulatedGroup):
             return False
         self._idx_buf = idx_example.clone()
         self._seed_dev = True

@@ -355,3 +355,41 @@ def test_weight_cache_layouts_match_torch(gpu):
             assert not fk[..., e["C"]:].any()
         if e["off_t"] >= 0:
             assert torch.equal(wc.dgrad(cv), krsc.permute(3, 1, 2, 0))
+
+
+def test_cuda_graph_emulated_fused_syncbn(gpu, tmp_path, monkeypatch):
+    """hipGraph replay of a step whose every BN runs the fused xGMI SyncBN exchange over 4
+    emulated ranks (SDX_SYNCBN_EMU=4): the exchange's epoch comes from device counters, so
+    each replay advances it. Graph replay follows the eager run over 5 steps (same batches):
+    parameters within reduction-order noise, BN running statistics close, no flag timeout."""
+    from simclr_pytorch_distributed_amd.config import parse_pretrain
+    from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+    from simclr_pytorch_distributed_amd.models.resnet import SupConResNet
+    from simclr_pytorch_distributed_amd.ops import _ext
+    monkeypatch.setenv("SDX_SYNCBN_EMU", "4")
+    monkeypatch.setenv("SDX_SYNCBN_EMU_KIND", "fused")
+    res = []
+    for graph in (False, True):
+        opt = parse_pretrain(["--batch_size", "32", "--synthetic", "--synthetic_size", "128", "--work_dir",
+                              str(tmp_path / f"e{int(graph)}"), "--model", "resnet18", "--backend", "native",
+                              "--learning_rate", "0.05", "--seed", "3"], make_dirs=False)
+        eng = PretrainEngine(opt)
+        assert eng.syncbn_transport == "emulated-4-fused"
+        torch.manual_seed(11)
+        eng.model.load_state_dict(SupConResNet("resnet18").state_dict())
+        idx = torch.arange(32, device=gpu)
+        if graph:
+            assert eng.enable_cuda_graph(idx)
+        w_init = eng.flat.flat.clone()
+        losses = []
+        for it in range(5):
+            st = eng.train_step(idx, 1, it, 10)
+            losses.append(float(st["loss_local"]))
+        torch.cuda.synchronize()
+        res.append((w_init, eng.flat.flat.clone(), eng.model.encoder.bn1.running_mean.clone(), losses))
+    (i0, w0, r0, l0), (i1, w1, r1, l1) = res
+    assert torch.equal(i0, i1)
+    rel = float((w0 - w1).norm() / (w0 - i0).norm())
+    assert rel < 2e-2, (rel, l0, l1)
+    assert torch.allclose(r0, r1, rtol=1e-3, atol=1e-4)
+    assert all(abs(a - b) < 1e-2 * max(1.0, abs(a)) for a, b in zip(l0, l1)), (l0, l1)
