@@ -52,6 +52,13 @@ const torch::Tensor& const_vec(const torch::Device& dev, int64_t n, float v) {
   return t;
 }
 
+// the head's GEMMs have few rows (one per view on this rank): the 64x64 tile is the only
+// one that puts enough blocks on the chip for their long reductions (512 rows, 2048 -> 2048:
+// 22.0 vs 28.6 us auto; 2048 -> 128: 15.5 us, profiles/head_gemm_r5.txt)
+int head_cfg(int64_t rows, int64_t ncol, int64_t kdim) {
+  return rows <= 2048 ? 3 : auto_cfg(rows, ncol, kdim, true);
+}
+
 ConvGeom gemm_geom(int64_t rows, int64_t in, int64_t out) {
   // a [rows] x [in] -> [out] GEMM as a 1x1 conv over `rows` single-pixel images
   ConvGeom g{};
@@ -70,7 +77,7 @@ torch::Tensor gemm_fwd(const torch::Tensor& x, const torch::Tensor& w, const tor
   auto y = torch::empty({rows, out}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   const GemmEpi epi{bias.data_ptr<float>(), relu ? 1 : 0, out_f32 ? 1 : 0};
   const ConvGeom g = gemm_geom(rows, in, out);
-  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), nullptr, auto_cfg(rows, out, in, true),
+  check_hip(launch_conv_fwd(g, x.data_ptr(), w.data_ptr(), y.data_ptr(), nullptr, head_cfg(rows, out, in),
                             cur_stream(), nullptr, nullptr, &epi),
             "head gemm_fwd");
   return y;
@@ -115,7 +122,7 @@ torch::Tensor gemm_dgrad(const torch::Tensor& dy, const torch::Tensor& wt, int64
   TORCH_CHECK(in % 8 == 0, "input features must be a multiple of 8");
   const ConvGeom g = gemm_geom(rows, in, out);
   // the masked-store statistics variant exists for the 64x64 LDS-DMA tile only (igemm.hip)
-  const int cfg = relu_ref != nullptr ? 3 : auto_cfg(rows, in, out, true);
+  const int cfg = relu_ref != nullptr ? 3 : head_cfg(rows, in, out);
   auto dx = torch::empty({rows, in}, dy.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   const GemmEpi epi{nullptr, 0, out_f32 ? 1 : 0};
   if (relu_ref == nullptr) {
