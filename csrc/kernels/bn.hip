@@ -13,6 +13,8 @@
 // bn_bwd_coef folds those into per-channel (A, D, E) so that dy = A·dz + D·y + E, plus
 // dγ/dβ; bn_bwd_apply is one elementwise pass producing dy (and dz for an identity
 // shortcut). All elementwise kernels move 8 bf16 (16 B) per lane.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 #include "bn_epilogue.h"
@@ -579,8 +581,14 @@ int ew_grid(long n8) {
 }  // namespace
 
 int col_reduce_gy(int rows) {
-  // balance the per-block row loop (rows/gy/4 trips) against the final combine (gy/4 loads)
-  int gy = (int)(sqrt((double)rows) / 2.0 + 0.5);
+  // balance the per-block row loop (rows/gy/4 trips) against the final combine (gy/4 loads);
+  // SDX_CR_GY scales the sqrt(rows) rule (A/B knob)
+  static const double scale = [] {
+    const char* e = getenv("SDX_CR_GY");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : 0.5;
+  }();
+  int gy = (int)(sqrt((double)rows) * scale + 0.5);
   if (gy > 64) gy = 64;
   if (gy < 1) gy = 1;
   return gy;
