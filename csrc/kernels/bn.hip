@@ -571,9 +571,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
 }
 
 int ew_grid(long n8) {
-  // enough lanes for SDX_EW_UNROLL elements each, at most 4096 blocks (2 per-CU residencies)
+  // enough lanes for SDX_EW_UNROLL elements each, at most 2048 blocks (one per-CU residency
+  // of 8 blocks; in-step 11.97 vs 12.04 ms/step at 4096, profiles/knob_revalidate_r5.txt).
+  // SDX_EW_BLOCKS overrides the cap, rounded to a multiple of 8 blocks (A/B knob)
+  static const long cap = [] {
+    const char* e = getenv("SDX_EW_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return v >= 8 ? v / 8 * 8 : 2048L;
+  }();
   long g = (n8 + 256L * SDX_EW_UNROLL - 1) / (256L * SDX_EW_UNROLL);
-  if (g > 4096) g = 4096;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
 }
