@@ -570,15 +570,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   }
 }
 
-int ew_grid(long n8) {
+int ew_grid(long n8, bool bwd = false) {
   // enough lanes for SDX_EW_UNROLL elements each, at most 2048 blocks (one per-CU residency
   // of 8 blocks; in-step 11.97 vs 12.04 ms/step at 4096, profiles/knob_revalidate_r5.txt).
-  // SDX_EW_BLOCKS overrides the cap, rounded to a multiple of 8 blocks (A/B knob)
-  static const long cap = [] {
-    const char* e = getenv("SDX_EW_BLOCKS");
+  // SDX_EW_BLOCKS overrides the cap, SDX_EW_BLOCKS_BWD that of bn_bwd_apply alone; rounded
+  // to a multiple of 8 blocks (A/B knobs)
+  auto env_cap = [](const char* name, long dflt) {
+    const char* e = getenv(name);
     const long v = e ? atol(e) : 0;
-    return v >= 8 ? v / 8 * 8 : 2048L;
-  }();
+    return v >= 8 ? v / 8 * 8 : dflt;
+  };
+  static const long cap_fwd = env_cap("SDX_EW_BLOCKS", 2048L);
+  static const long cap_bwd = env_cap("SDX_EW_BLOCKS_BWD", cap_fwd);
+  const long cap = bwd ? cap_bwd : cap_fwd;
   long g = (n8 + 256L * SDX_EW_UNROLL - 1) / (256L * SDX_EW_UNROLL);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
@@ -722,11 +726,11 @@ hipError_t launch_bn_bwd_apply(const void* dout, const void* outv, const void* y
   const long n8 = numel / 8;
   const int C8 = C / 8;
   if (yb)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(ew_grid(n8, true)), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)yb, cb, (uint16_t*)dya,
                        (uint16_t*)dyb, (uint16_t*)dz_out, n8, C8, C, msc, msh, (const uint8_t*)omask);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(ew_grid(n8)), dim3(256), 0, s, (const uint16_t*)dout,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(ew_grid(n8, true)), dim3(256), 0, s, (const uint16_t*)dout,
                        (const uint16_t*)outv, (const uint16_t*)ya, ca, (const uint16_t*)nullptr, (const float*)nullptr,
                        (uint16_t*)dya, (uint16_t*)nullptr, (uint16_t*)dz_out, n8, C8, C, msc, msh,
                        (const uint8_t*)omask);
