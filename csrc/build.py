@@ -125,7 +125,12 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         results = list(ex.map(lambda t: job(*t), tasks))
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
-    if (rebuilt or force or not os.path.exists(out_so)
+    # the object set the .so was linked from: a source reverted to content whose object is
+    # still cached rebuilds nothing and leaves the .so newer than every object, so an mtime
+    # test alone would keep the stale link
+    stamp = out_so + ".objs"
+    linked = open(stamp).read() if os.path.exists(stamp) else ""
+    if (rebuilt or force or not os.path.exists(out_so) or linked != "\n".join(objs)
             or os.path.getmtime(out_so) < max(os.path.getmtime(o) for o in objs)):
         libs = []
         for p in lib_torch:
@@ -141,6 +146,8 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, out_so)
+        with open(stamp, "w") as fh:
+            fh.write("\n".join(objs))
     return out_so
 
 
