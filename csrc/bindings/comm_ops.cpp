@@ -157,9 +157,15 @@ void sweep() {
     const hipError_t q = hipEventQuery(c->ev);
     if (q == hipSuccess) {
       continue;
+    } else if (q == hipErrorCapturedEvent) {
+      // the event was last recorded inside a stream capture (arm() skips capturing streams,
+      // so only a record from before that rule could do this): it keeps refusing queries,
+      // so its deadline could never fire -- disarm; the next eager collective re-arms it
+      c->armed.store(false, std::memory_order_release);
+      continue;
     } else if (q >= hipErrorStreamCaptureUnsupported && q <= hipErrorStreamCaptureWrongThread) {
-      // a stream capture (hipGraph) in progress on another thread refuses the query: no
-      // verdict this sweep (the deadline keeps running from the armed record)
+      // a global-mode capture in progress refuses the query: no verdict this sweep (the
+      // deadline keeps running from the armed record)
       continue;
     } else if (q == hipErrorNotReady) {
       const double waited = 1e-9 * (double)(now_ns() - c->armed_at.load());
@@ -221,6 +227,11 @@ void ensure_watchdog() {
 void arm(SmallComm& c, hipStream_t s) {
   c.ops.fetch_add(1, std::memory_order_relaxed);
   if (c.world <= 1) return;
+  // a collective captured into a hipGraph: an event recorded here would become a graph node
+  // and, queried later, refuse with hipErrorCapturedEvent; replays are watched by the next
+  // eager collective's record (or the c10d watchdog)
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;
   const int64_t t = now_ns();
   if (c.armed.load(std::memory_order_acquire) && t - c.armed_at.load() < 200000) return;
   c.armed_at.store(t);

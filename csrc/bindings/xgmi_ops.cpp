@@ -28,7 +28,34 @@ struct Arena {
   int* err = nullptr;              // host-pinned, GPU-written error word (sender index + 1)
   long long timeout_ticks = 0;     // flag-poll deadline in 100 MHz wall-clock ticks
   double ticks_per_s = 1e8;        // wall-clock rate
+  // Stream-order invariant of the device epoch (bn.hip XgmiCol::epoch_ctr): a launch reads
+  // ctr + 1 at its start and stores it back at its end, so two launches on one arena must
+  // never overlap -- they would read the same epoch / flag parity and could pass on each
+  // other's flags. Every call is issued on the stream of the previous one, or (order_on) the
+  // new stream first waits for the previous stream's work.
+  hipStream_t last_stream = nullptr;
+  hipEvent_t order_ev = nullptr;
 };
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// serialise arena use across streams (see Arena::last_stream). Inside a stream capture the
+// capturing code orders its streams itself (torch.cuda.graph warm-up / capture streams
+// wait on the previous stream), and an event node must not leak into the graph, so no event
+// is recorded or waited then. Streams come from torch's pool, which never destroys them.
+void order_on(Arena& a, hipStream_t s) {
+  if (a.last_stream == s) return;
+  if (a.last_stream != nullptr && !capturing(s) && !capturing(a.last_stream)) {
+    if (a.order_ev == nullptr)
+      check_hip(hipEventCreateWithFlags(&a.order_ev, hipEventDisableTiming), "hipEventCreate(arena order)");
+    check_hip(hipEventRecord(a.order_ev, a.last_stream), "hipEventRecord(arena order)");
+    check_hip(hipStreamWaitEvent(s, a.order_ev, 0), "hipStreamWaitEvent(arena order)");
+  }
+  a.last_stream = s;
+}
 
 // a per-call deadline (start-up self-checks: seconds, not --comm_timeout) capped by the arena's
 long long call_ticks(const Arena& a, double timeout_s) {
@@ -120,6 +147,7 @@ torch::Tensor xgmi_allreduce(int64_t id, torch::Tensor x, double timeout_s) {
   TORCH_CHECK((size_t)x.numel() <= a.cap, "message larger than the arena slot");
   c10::DeviceGuard dg(x.device());
   auto out = torch::empty_like(x);
+  order_on(a, cur_stream());
   a.epoch += 1;
   check_hip(launch_xgmi_allreduce(x.data_ptr<double>(), out.data_ptr<double>(), (int)x.numel(), a.peers, a.rank,
                                   a.world, a.epoch, a.err, call_ticks(a, timeout_s), cur_stream(), a.epoch_dev),
@@ -144,6 +172,7 @@ void xgmi_destroy(int64_t id) {
   (void)hipFree(a->base);
   (void)hipFree(a->epoch_dev);
   (void)hipHostFree(a->err);
+  if (a->order_ev != nullptr) (void)hipEventDestroy(a->order_ev);
 }
 
 // W virtual ranks on this device (single-GPU emulation of the fused SyncBN exchange, the
@@ -221,6 +250,7 @@ torch::Tensor xgmi_emulate(torch::Tensor in, int64_t iters) {
 // (epoch advanced; mode 1 real peers, 2 emulated ranks)
 XgmiCol xgmi_col_args(int64_t id) {
   Arena& a = get(id);
+  order_on(a, cur_stream());
   XgmiCol x{};
   x.peers = a.peers;
   x.mode = a.emulated ? 2 : 1;

@@ -71,11 +71,17 @@ def _add_common_new_flags(p: argparse.ArgumentParser):
     g.add_argument("--max_steps", type=int, default=0, help="stop each epoch after this many steps (0 = all)")
     g.add_argument("--gpu_aug", type=int, default=1,
                    help="augmentation on the GPU kernel (1) or the CPU torch pipeline on --num_workers threads (0)")
-    g.add_argument("--syncbn_comm", type=str, default="auto", choices=["auto", "rccl", "xgmi"],
-                   help="SyncBN statistics exchange: auto (default: set up every transport the job can have "
-                        "-- the fused one-shot xGMI exchange when every rank is on one node, a dedicated RCCL "
-                        "communicator -- and keep the one measured fastest on the first batch, agreed by all "
-                        "ranks), rccl, xgmi (forced; RCCL is the fallback when the arena's self-check fails)")
+    # default rccl: the fused xGMI exchange has only ever run as same-device IPC
+    # rehearsals (several processes on one GPU, emulated ranks); its peer stores and flag
+    # protocol have not yet executed across real xGMI links, so it is opt-in until they have
+    g.add_argument("--syncbn_comm", type=str, default="rccl", choices=["auto", "rccl", "xgmi"],
+                   help="SyncBN statistics exchange: rccl (default: a dedicated RCCL communicator, "
+                        "reduce -> ncclAllReduce -> finalize per BN), xgmi (the fused one-shot xGMI exchange, "
+                        "every rank on one node; RCCL is the fallback when the arena's self-check fails), "
+                        "auto (set up both and keep the one measured fastest on the first batch, agreed by "
+                        "all ranks). xgmi/auto are EXPERIMENTAL: the fused exchange has been validated on "
+                        "one GPU (multi-process IPC rehearsals, emulated ranks) but not yet across real "
+                        "peer GPUs")
     g.add_argument("--comm_timeout", type=float, default=600.0,
                    help="collective timeout in seconds (a dead/stalled peer raises instead of hanging)")
     g.add_argument("--profile", action="store_true",

@@ -662,6 +662,11 @@ class PretrainEngine:
                     sys.stdout.flush()
                 window_loss = torch.zeros((), device=self.device)
                 window_n = 0
+        # BN num_batches_tracked is host-counted on the native path: visible in the buffers
+        # from every epoch end on, not only through state_dict()
+        flush = getattr(self.runner, "flush_bn_counters", None)
+        if flush is not None:
+            flush()
         return losses.avg
 
     def run(self):

@@ -117,8 +117,18 @@ class ModelRunner:
         # buffers when something reads them (state_dict: checkpoints, evaluation copies) — no
         # per-step kernel for a counter the training math never reads (momentum is set)
         self._nbt_pending = 0
-        if hasattr(model, "register_state_dict_pre_hook"):
-            model.register_state_dict_pre_hook(lambda *a, **k: self.flush_bn_counters())
+        # flushed before any state_dict() / load_state_dict() that reaches a BN, called on the
+        # top-level model or on any submodule (e.g. model.encoder): the hooks sit on every BN
+        # module. A load flushes first, so the loaded counters replace the flushed ones instead
+        # of having the pending count added on top later. Direct reads of
+        # bn.num_batches_tracked between flushes see the last flushed value (the engines flush
+        # at every epoch end).
+        for m in model.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                if hasattr(m, "register_state_dict_pre_hook"):
+                    m.register_state_dict_pre_hook(lambda *a, **k: self.flush_bn_counters())
+                if hasattr(m, "register_load_state_dict_pre_hook"):
+                    m.register_load_state_dict_pre_hook(lambda *a, **k: self.flush_bn_counters())
 
     def weight_cache(self):
         if self._wc is None:

@@ -279,7 +279,7 @@ def create_rccl_small_comm(group=None, timeout_s: float = 600.0) -> int:
             st["uid"] = m.rccl_unique_id()
 
     def share():
-        t = st["uid"].to(dev) if backend() == "nccl" else st["uid"]
+        t = st["uid"].to(dev) if dist.get_backend(group) == "nccl" else st["uid"]
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         st["uid"] = t.cpu()
 

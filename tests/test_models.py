@@ -31,3 +31,22 @@ def test_forward_shapes():
     assert SupCEResNet("resnet18", 10)(torch.randn(2, 3, 32, 32)).shape == (2, 10)
     assert LinearClassifier("resnet50", 100)(torch.randn(2, 2048)).shape == (2, 100)
     assert SupConResNet("resnet18", stem="imagenet")(torch.randn(2, 3, 64, 64)).shape == (2, 128)
+
+
+def test_host_counted_bn_passes_flush_on_submodule_state_dict_and_load():
+    """The native runner counts BN training passes on the host (models/executor.py): a
+    state_dict() of a SUBMODULE flushes them, and a load_state_dict() flushes first so the
+    loaded counters replace them instead of having the pending count added later."""
+    from simclr_pytorch_distributed_amd.models.executor import ModelRunner
+    m = SupConResNet("resnet18")
+    r = ModelRunner(m, "native", fused=True)
+    r._nbt = [b.num_batches_tracked for b in m.encoder.modules() if isinstance(b, torch.nn.BatchNorm2d)]
+    r._nbt_pending = 3
+    sd = {k: v.clone() for k, v in m.encoder.state_dict().items()}
+    assert int(sd["bn1.num_batches_tracked"]) == 3 and r._nbt_pending == 0
+    r._nbt_pending = 2
+    sd["bn1.num_batches_tracked"].fill_(7)
+    m.encoder.load_state_dict(sd)
+    assert r._nbt_pending == 0
+    assert int(m.encoder.bn1.num_batches_tracked) == 7
+    assert int(m.state_dict()["encoder.bn1.num_batches_tracked"]) == 7

@@ -113,3 +113,83 @@ def test_agree_fastest_single_process():
     from simclr_pytorch_distributed_amd.parallel import comm
     best, red = comm.agree_fastest(["a", "b", "c"], [3.0, 2.0, 2.0])
     assert best == "b" and red == [3.0, 2.0, 2.0]
+
+
+def _setup_entry(rank, world, port, d, want, xgmi_fail, rccl_fail):
+    """PretrainEngine._setup_syncbn_comm on a stub engine, with the native extension
+    replaced by a fake whose xGMI arena creation / RCCL communicator join raise on ONE rank;
+    comm.backend() reports nccl so the RCCL candidate is attempted (the uid broadcast runs
+    on the gloo group itself)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    import datetime
+    import types
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        from simclr_pytorch_distributed_amd.engine.pretrain import PretrainEngine
+        from simclr_pytorch_distributed_amd.ops import _ext
+        from simclr_pytorch_distributed_amd.parallel import comm
+        log = []
+
+        def xgmi_create(r, w, cap, t):
+            if rank == xgmi_fail:
+                raise RuntimeError("injected: arena allocation failed")
+            log.append("xgmi_create")
+            return 3
+
+        def rccl_comm_init(uid, w, r, t):
+            if rank == rccl_fail:
+                raise RuntimeError("injected: ncclCommInitRank failed")
+            log.append("rccl_init")
+            return 7
+
+        fake = types.SimpleNamespace(
+            xgmi_create=xgmi_create, xgmi_handle=lambda i: torch.zeros(64, dtype=torch.uint8),
+            xgmi_open=lambda i, h: (_ for _ in ()).throw(RuntimeError("no peer mapping on the CPU")),
+            xgmi_destroy=lambda i: log.append(f"xgmi_destroy{i}"),
+            small_comm_destroy=lambda h: log.append(f"comm_destroy{h}"),
+            rccl_unique_id=lambda: torch.arange(128, dtype=torch.uint8),
+            rccl_comm_init=rccl_comm_init,
+            small_comm_abort=lambda h: log.append(f"abort{h}"))
+        _ext.require = lambda: fake
+        comm.backend = lambda: "nccl"
+        torch.cuda.current_device = lambda: 0
+        stub = types.SimpleNamespace(syncbn_transport="none")
+        stub._activate_syncbn = lambda name: PretrainEngine._activate_syncbn(stub, name)
+        opt = types.SimpleNamespace(syncbn_comm=want, comm_timeout=30.0)
+        PretrainEngine._setup_syncbn_comm(stub, opt, torch.device("cuda"))
+        with open(os.path.join(d, f"r{rank}.txt"), "w") as f:
+            f.write(f"{stub.syncbn_transport} {','.join(stub._syncbn_cands) or '-'} {','.join(log) or '-'}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,want,xgmi_fail,rccl_fail,expect", [
+    (2, "rccl", -1, 1, "none"),          # the RCCL join fails on rank 1: every rank falls back
+    (4, "rccl", -1, 2, "none"),
+    (2, "auto", 0, 1, "none"),           # both candidates fail, on different ranks
+    # the xGMI arena fails on rank 3: every rank destroys its arena and joins RCCL together
+    # (whose GPU self-check then fails everywhere alike: no GPU in this container)
+    (4, "auto", 3, -1, "none"),
+])
+def test_syncbn_setup_falls_back_together(world, want, xgmi_fail, rccl_fail, expect):
+    """a candidate transport whose creation raises on ONE rank during
+    _setup_syncbn_comm leaves every rank with the same transport (no rank inside a
+    collective alone: a hang would fail the spawn join), and a rank that had created its
+    own handle before the failure aborts it."""
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_setup_entry, args=(world, port, d, want, xgmi_fail, rccl_fail), nprocs=world, join=True)
+        res = [open(os.path.join(d, f"r{r}.txt")).read().split(" ") for r in range(world)]
+    for r, (transport, cands, log) in enumerate(res):
+        assert transport == expect, (r, transport, cands, log)
+        if expect == "none":
+            assert cands == "-", (r, cands)
+            if want == "rccl" or rccl_fail >= 0:
+                # the ranks that joined aborted their handle; the failing rank never had one
+                assert ("abort7" in log) == (r != rccl_fail), (r, log)
+        if xgmi_fail >= 0 and r != xgmi_fail:
+            assert "xgmi_destroy3" in log, (r, log)   # arena created, then destroyed together
+        if rccl_fail < 0:
+            assert log.count("rccl_init") == 1 and log.endswith("abort7"), (r, log)
