@@ -437,6 +437,24 @@ void keep_deferred_partial(const torch::Tensor& part) {
   if (part.defined() && splitk_deferring(cur_stream())) side_stash().push_back(part);
 }
 
+// block target of the dedicated 1x1 / 3x3 wgrad kernels' split heuristic: SDX_W3_BLOCKS
+// (default 128, half the chip: the eager step runs them on the side stream beside the
+// critical path). A step captured as one hipGraph chain runs them alone, in line, so
+// PretrainEngine.enable_cuda_graph raises it to the whole chip for the capture
+// (wgrad_block_target_set).
+std::atomic<int64_t>& wgrad_block_target_ref() {
+  static std::atomic<int64_t> t{[] {
+    const char* e = getenv("SDX_W3_BLOCKS");
+    return e ? atoll(e) : 128LL;
+  }()};
+  return t;
+}
+int64_t wgrad_block_target() { return wgrad_block_target_ref().load(std::memory_order_relaxed); }
+int64_t wgrad_block_target_set(int64_t n) {
+  TORCH_CHECK(n >= 1 && n <= 4096, "block target in [1, 4096]");
+  return wgrad_block_target_ref().exchange(n);
+}
+
 torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                          int64_t splits, int64_t cfg, c10::optional<torch::Tensor> out, bool accumulate,
                          OptT in_scale, OptT in_shift) {
@@ -495,10 +513,7 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
     // as for the 3x3 kernel: SDX_W3_BLOCKS (128) 8-wave blocks, >= 8 steps each
     const int64_t steps = wgrad1x1_steps(g);
     if (splits <= 0) {
-      static const int64_t target0 = [] {
-        const char* e = getenv("SDX_W3_BLOCKS");
-        return e ? atoll(e) : 128LL;
-      }();
+      const int64_t target0 = wgrad_block_target();
       // pixel-pair shapes (HBM-bound, twice the MFMA work per byte): SDX_W1_PAIR_BLOCKS
       static const int64_t pair_target = [] {
         const char* e = getenv("SDX_W1_PAIR_BLOCKS");
@@ -518,10 +533,7 @@ torch::Tensor conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t R, int64_t S
       // so the critical-path kernels (128-VGPR dgrads, the BN reductions) cannot co-reside on
       // its CU. 128 blocks leave half the CUs to the main stream: step 13.71 -> 13.34 ms at
       // 256 images/GPU, 8.48 -> 8.20 ms at 128 (profiles/wgrad3x3_r2.txt)
-      static const int64_t target0 = [] {
-        const char* e = getenv("SDX_W3_BLOCKS");
-        return e ? atoll(e) : 128LL;
-      }();
+      const int64_t target0 = wgrad_block_target();
       const int64_t target = tail ? tail_blocks : target0;
       const int64_t tiles = wgrad3x3_tiles(g), steps = wgrad3x3_steps(g);
       splits = std::max<int64_t>(1, target / tiles);
@@ -1718,6 +1730,11 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("relu"));
   m.def("wgrad1x1_pairs_set", [](int64_t on) { return (int64_t)wgrad1x1_pairs_set((int)on); },
         "pixel-pair 1x1 wgrad for 64-channel sides on (1) / off (0); returns the previous value", pybind11::arg("on"));
+  m.def("wgrad_block_target_set", &wgrad_block_target_set,
+        "block target of the dedicated 1x1/3x3 wgrad kernels' split heuristic (SDX_W3_BLOCKS); returns the previous value",
+        pybind11::arg("n"));
+  m.def("wgrad1x1_big_set", [](int64_t on) { return (int64_t)wgrad1x1_big_set((int)on); },
+        "256-row LDS-DMA 1x1 wgrad kernel on (1) / off (0); returns the previous value", pybind11::arg("on"));
   m.def("tap3_set", &tap3_set,
         "tap-reuse 3x3 conv loop on (1) / off (0) for auto tile selection; returns the previous value",
         pybind11::arg("on"));

@@ -481,6 +481,199 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256-row LDS-DMA variant (default for K % 256 == 0; SDX_W1_BIG=0 restores the kernels
+// above). The kernels above move 24 KB of operands per 32-pixel step for a 128 x 256 output
+// tile through a 4-deep register ring, and per CU they stream at ~48 GB/s even with the
+// chip to themselves (32 blocks: 1000 cycles per step against 512 of MFMA work,
+// profiles/w1_split_r6.txt): one block per CU, ~96 KB in flight, the L2 misses of a step
+// (the first tile to touch a pixel range fetches it from HBM) are latency-bound. Here a
+// block owns a 256 x BN tile (BN = 256, or 128), so a step's 32 KB feed twice the MFMA
+// work (1.5x fewer operand bytes per FLOP), and the operands are staged by LDS-DMA
+// (global_load_lds_dwordx4) into a 4-slot ring with THREE steps in flight across every
+// barrier (no staging registers: 128 accumulator + 48 fragment VGPRs fit two waves per
+// SIMD).
+//
+// LDS image: the same K-outer chunk swizzle as above (w1_off), so the fragment reads are
+// the transposed ds_read_b64_tr_b16 pair of the kernels above. LDS-DMA writes a wave's
+// 64 x 16 B linearly, so the swizzle moves to the SOURCE: the lane that lands in chunk
+// slot s of row r fetches logical chunk s ^ swz(r) (cdna_hip_programming.md §5, rule 21).
+// Per 32-pixel step: A = dy [32][256] (16 KiB, 16 wave-DMAs), B = x [32][BN] (16 or 8).
+//
+// Loop (step k in slot k % 4): see the pipeline note at the loop; three steps' DMAs are in
+// flight under every step's MFMAs.
+// No other vector-memory instruction runs in the loop, so the counted vmcnt is exact, and
+// the barrier is the raw s_barrier (a __syncthreads() would drain the ring, vmcnt(0)).
+// Steps past the split's end DMA the zero page into their (never read) slot, keeping the
+// per-iteration DMA count uniform.
+constexpr int W1B_BM = 256;
+constexpr int W1B_NS = 4;   // LDS slots
+
+__device__ __forceinline__ void w1_glds16(w1_gptr src, void* lds) {
+  asm volatile("" : "+v"(src));   // one DMA per select (no duplicated exec-masked branches)
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void w1_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void w1_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BN>
+__global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_big_kernel(W1Params p) {
+  constexpr int A_BYTES = 32 * W1B_BM * 2;             // 16 KiB
+  constexpr int B_BYTES = 32 * BN * 2;                 // 16 / 8 KiB
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int ND_A = A_BYTES / 1024 / 8;             // DMAs per wave per step: 2
+  constexpr int ND_B = B_BYTES / 1024 / 8;             // 2 / 1
+  constexpr int ND = ND_A + ND_B;
+  constexpr int A_CPR = W1B_BM / 8, B_CPR = BN / 8;     // 16-B chunks per image row
+  constexpr int A_RPD = 64 / A_CPR, B_RPD = 64 / B_CPR; // image rows per wave-DMA
+  constexpr int WN_COLS = BN / 4, TN = WN_COLS / 16;   // wave tile 128 x BN/4
+  constexpr int TM = 8;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[W1B_NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h4 = lane >> 4, c16 = lane & 15;
+  const int wm = wv >> 2, wn = wv & 3;
+
+  const int tiles = p.k_tiles * p.c_tiles;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lin % tiles, split = lin / tiles;
+  const int k0 = (tile / p.c_tiles) * W1B_BM, c0 = (tile % p.c_tiles) * BN;
+  const int s_begin = split * p.steps_per_split;
+  const int s_end = min(p.steps_total, s_begin + p.steps_per_split);
+
+  // ---- DMA sources (32-bit element offsets of step 0; host check P*K, H*W*C < 2^31) ----
+  int a_src[ND_A], b_src[ND_B];
+#pragma unroll
+  for (int i = 0; i < ND_A; ++i) {
+    const int d = wv * ND_A + i;                     // wave-DMA index within the A image
+    const int r = d * A_RPD + lane / A_CPR, s = lane % A_CPR;
+    a_src[i] = r * p.K + k0 + ((s ^ kout_swz_w1<W1B_BM>(r)) << 3);
+  }
+#pragma unroll
+  for (int i = 0; i < ND_B; ++i) {
+    const int d = wv * ND_B + i;
+    const int r = d * B_RPD + lane / B_CPR, s = lane % B_CPR;
+    const int xp = p.xst * (p.xw * (r / p.xq) + r % p.xq);
+    b_src[i] = xp * p.C + c0 + ((s ^ kout_swz_w1<BN>(r)) << 3);
+  }
+  const int sA = 32 * p.K, sB = p.x_step;
+  w1_gptr zp = (w1_gptr)w1_zero16;
+  asm volatile("" : "+s"(zp));
+  const w1_gptr gdy = (w1_gptr)p.dy, gx = (w1_gptr)p.x;
+  auto issue = [&](int step) __attribute__((always_inline)) {
+    const bool ok = step < s_end;
+    unsigned char* st = smem + (step % W1B_NS) * STAGE;
+#pragma unroll
+    for (int i = 0; i < ND_A; ++i)
+      w1_glds16(ok ? gdy + (a_src[i] + step * sA) : zp, st + (wv * ND_A + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < ND_B; ++i)
+      w1_glds16(ok ? gx + (b_src[i] + step * sB) : zp, st + A_BYTES + (wv * ND_B + i) * 1024);
+  };
+
+  // ---- fragment offsets (as wgrad1x1_pipe_kernel) ----
+  const int q = c16 >> 2, pp = c16 & 3;
+  const int p_lo = 8 * h4 + q;
+  auto kout = [&](auto cols_tag, int row, int col0) __attribute__((always_inline)) {
+    constexpr int COLS = decltype(cols_tag)::value;
+    const int col = col0 + 4 * pp;
+    return w1_off<COLS>(row, col >> 3) + (col & 7) * 2;
+  };
+  // LDS byte addresses of stage 0 (a stage adds k % 4 · STAGE)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)smem;
+  uint32_t ao[TM], bo[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) ao[i] = lds0 + kout(std::integral_constant<int, W1B_BM>{}, p_lo, wm * 128 + 16 * i);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bo[j] = lds0 + A_BYTES + kout(std::integral_constant<int, BN>{}, p_lo, wn * WN_COLS + 16 * j);
+  // The transposed fragment reads are inline asm: issued through the builtin, every one of
+  // them is ordered by hipcc behind ALL pending LDS-DMAs (it cannot tell that they target
+  // another slot) -- an s_waitcnt vmcnt(0) at the top of each step that drains the ring. In
+  // asm the compiler neither waits for them, so each use is preceded by a counted lgkmcnt
+  // (LDS returns in order; the loop issues no scalar loads) that also names the fragment as
+  // an operand, pinning the MFMAs behind it. pixel row p_hi = p_lo + 4 is a constant
+  // 4·COLS·2 bytes further (the swizzle ignores row bit 2).
+  auto frag = [&](uint32_t a, auto cols_tag) __attribute__((always_inline)) -> bf16x8 {
+    constexpr int HI = 4 * decltype(cols_tag)::value * 2;
+    bf16x4 lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a), "i"(HI));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Software-pipelined over two named fragment sets: iteration k waits for step k+1's DMA,
+  // passes the barrier (its lgkmcnt(0) also completes step k's fragment reads, issued one
+  // iteration earlier), issues step k+1's fragment reads and step k+4's DMA into step k's
+  // slot (every wave has finished reading it: the barrier), then runs step k's MFMAs on the
+  // fragments in registers -- the reads and the DMA fly under the MFMAs. The fragments are
+  // tied behind the barrier by empty asm so no MFMA is scheduled above its wait.
+  auto read_set = [&](int k, bf16x8 (&fa)[TM], bf16x8 (&fb)[TN]) __attribute__((always_inline)) {
+    const uint32_t st = (uint32_t)((k % W1B_NS) * STAGE);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = frag(bo[j] + st, std::integral_constant<int, BN>{});
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] = frag(ao[i] + st, std::integral_constant<int, W1B_BM>{});
+  };
+  auto iter = [&](int k, bf16x8 (&ca)[TM], bf16x8 (&cb)[TN], bf16x8 (&na)[TM], bf16x8 (&nb)[TN])
+      __attribute__((always_inline)) {
+    w1_vm_wait<2 * ND>();
+    w1_lds_barrier();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(ca[i]));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(cb[j]));
+    read_set(k + 1, na, nb);
+    issue(k + 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], ca[i], acc[i][j], 0, 0, 0);
+  };
+  bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  issue(s_begin);
+  issue(s_begin + 1);
+  issue(s_begin + 2);
+  issue(s_begin + 3);
+  w1_vm_wait<3 * ND>();
+  w1_lds_barrier();
+  read_set(s_begin, fa0, fb0);
+  for (int k = s_begin; k < s_end; k += 2) {
+    iter(k, fa0, fb0, fa1, fb1);
+    if (k + 1 < s_end) iter(k + 1, fa1, fb1, fa0, fb0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the last (unused) fragment reads
+  w1_vm_wait<0>();   // the tail DMAs (zero page) land before the block's LDS is released
+
+  float* out = p.part + (size_t)split * p.K * p.C;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = k0 + wm * 128 + 16 * i + c16;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = c0 + wn * WN_COLS + 16 * j + 4 * h4;
+      const f32x4 a = acc[i][j];
+      st16<SDX_NT_PART != 0>(out + (size_t)m * p.C + n,
+                             make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]),
+                                        __float_as_uint(a[3])));
+    }
+  }
+}
+
 // SDX_W1_BN=128 forces the 128-column tile on every shape (co-residency experiments: the
 // non-pipelined 128x128 kernel holds 112 VGPRs, so an 8-wave main-stream block fits beside it)
 // pixel-pair view (stride 1, a 64-channel side: the layer-1 bottleneck 1x1 convs, reference
@@ -506,6 +699,22 @@ bool w1_pairs(const ConvGeom& g) {
 }
 int w1_kv(const ConvGeom& g) { return w1_pairs(g) ? 2 * g.K : g.K; }
 int w1_cv(const ConvGeom& g) { return w1_pairs(g) ? 2 * g.C : g.C; }
+
+// the 256-row LDS-DMA kernel: dy channels % 256, the non-GEN x addressing (stride 1, or a
+// strided shortcut whose 32-pixel step is whole output rows), not the pixel-pair view.
+// SDX_W1_BIG=0: the 128-row kernels for every shape
+bool w1_pipe_enabled(const ConvGeom& g);
+std::atomic<int>& w1_big_flag() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("SDX_W1_BIG");
+    return e == nullptr || atoi(e) != 0 ? 1 : 0;
+  }()};
+  return on;
+}
+bool w1_big(const ConvGeom& g) {
+  return w1_big_flag().load(std::memory_order_relaxed) != 0 && !w1_pairs(g) && g.K % W1B_BM == 0 && g.C % 128 == 0 && w1_pipe_enabled(g) &&
+         (g.stride == 1 || 32 % g.Q == 0);
+}
 
 int wgrad1x1_bn(const ConvGeom& g) {
   static const int force = [] {
@@ -545,7 +754,10 @@ bool wgrad1x1_supported(const ConvGeom& g) {
          g.K % W1_BM == 0 && g.C % 128 == 0 && ((long)g.N * g.P * g.Q) % 32 == 0;
 }
 
-int wgrad1x1_tiles(const ConvGeom& g) { return (w1_kv(g) / W1_BM) * (w1_cv(g) / wgrad1x1_bn(g)); }
+int wgrad1x1_tiles(const ConvGeom& g) {
+  if (w1_big(g)) return (g.K / W1B_BM) * (g.C / wgrad1x1_bn(g));
+  return (w1_kv(g) / W1_BM) * (w1_cv(g) / wgrad1x1_bn(g));
+}
 
 int wgrad1x1_steps(const ConvGeom& g) { return (int)((long)g.N * g.P * g.Q / (w1_pairs(g) ? 64 : 32)); }
 
@@ -554,6 +766,8 @@ int wgrad1x1_slices(const ConvGeom& g, int splits) { return w1_pairs(g) ? 2 * sp
 bool wgrad1x1_pair_view(const ConvGeom& g) { return w1_pairs(g); }
 
 int wgrad1x1_pairs_set(int on) { return w1_pairs_flag().exchange(on ? 1 : 0); }
+
+int wgrad1x1_big_set(int on) { return w1_big_flag().exchange(on ? 1 : 0); }
 
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s) {
@@ -578,13 +792,17 @@ hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, flo
   p.steps_per_split = (p.steps_total + splits - 1) / splits;
   p.splits = (p.steps_total + p.steps_per_split - 1) / p.steps_per_split;
   const int bn = wgrad1x1_bn(g);
-  p.k_tiles = p.K / W1_BM;
+  const bool big = w1_big(g);
+  p.k_tiles = p.K / (big ? W1B_BM : W1_BM);
   p.c_tiles = p.C / bn;
   const bool direct = p.splits == 1 && !accumulate && !p.pairs;
   if (!direct && partial == nullptr) return hipErrorInvalidValue;
   p.part = direct ? dw : partial;
   const dim3 grid(p.k_tiles * p.c_tiles * p.splits), block(W1_NT);
-  if (w1_pipe_enabled(g)) {   // (a strided shape is supported only when it is)
+  if (big) {
+    if (bn == 256) hipLaunchKernelGGL(wgrad1x1_big_kernel<256>, grid, block, 0, s, p);
+    else hipLaunchKernelGGL(wgrad1x1_big_kernel<128>, grid, block, 0, s, p);
+  } else if (w1_pipe_enabled(g)) {   // (a strided shape is supported only when it is)
     const bool gen = g.stride > 1 && 32 % g.Q != 0;
     if (gen) {
       if (bn == 256) hipLaunchKernelGGL((wgrad1x1_pipe_kernel<256, true>), grid, block, 0, s, p);

@@ -521,18 +521,37 @@ class PretrainEngine:
         snap = [t.detach().clone() for t in state]
         pend = self.runner._nbt_pending
         self._host_prelude(1, 0, 1)
-        s = torch.cuda.Stream(device=self.device)
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self._step_body(self._idx_buf)
-        torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        p0 = self.runner._nbt_pending
-        # thread-local capture: the communicator watchdog thread (csrc/bindings/comm_ops.cpp)
-        # keeps polling its events while this thread captures
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self._graph_stats = self._step_body(self._idx_buf)
+        # The step is captured as ONE chain: the weight gradients run in line on the capture
+        # stream instead of forking to the wgrad side stream (SDX_GRAPH_SIDE=1 keeps the
+        # fork). A captured two-stream DAG replays its branches on several hardware queues
+        # with no stream priority and a cross-queue wait at every fork: 24.9 vs 11.9 ms
+        # eager at 256 images/GPU, while each kernel replayed on its own runs at its eager
+        # speed (profiles/graph_probe_r6.txt).
+        # In line, the dedicated wgrad kernels get the whole chip (their eager block target
+        # keeps half of it for the concurrent critical path): SDX_GRAPH_WGRAD_BLOCKS, 256.
+        from ..ops import _ext, streams
+        side_prev = streams.ENABLED
+        streams.ENABLED = os.environ.get("SDX_GRAPH_SIDE", "0") == "1"
+        m = _ext.require()
+        tgt_prev = m.wgrad_block_target_set(int(os.environ.get("SDX_GRAPH_WGRAD_BLOCKS", "256"))) \
+            if not streams.ENABLED else None
+        try:
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    self._step_body(self._idx_buf)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            p0 = self.runner._nbt_pending
+            # thread-local capture: the communicator watchdog thread (csrc/bindings/comm_ops.cpp)
+            # keeps polling its events while this thread captures
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._graph_stats = self._step_body(self._idx_buf)
+        finally:
+            streams.ENABLED = side_prev
+            if tgt_prev is not None:
+                m.wgrad_block_target_set(tgt_prev)
         # BN passes of one step, counted on the host (ModelRunner.flush_bn_counters) per replay
         self._graph_nbt = self.runner._nbt_pending - p0
         self._graph = g

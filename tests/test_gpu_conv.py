@@ -447,3 +447,33 @@ def test_conv_dgrad_cat(gpu, shape, cfg):
     d = dx.double().reshape(-1, C)
     assert torch.allclose(s[0], d.sum(0), rtol=1e-4, atol=1e-2)
     assert torch.allclose(s[1], (d * (ya.double().reshape(-1, C) - ma.double())).sum(0), rtol=1e-4, atol=1e-1)
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 512, 256), (8, 4, 128, 512), (16, 16, 256, 256), (4, 8, 2048, 512),
+                                   (3, 8, 256, 768)])
+@pytest.mark.parametrize("splits", [1, 5, 0])
+def test_wgrad1x1_big_matches_128row_kernel(gpu, shape, splits):
+    """The 256-row LDS-DMA 1x1 wgrad (wgrad1x1_big_kernel: 4-slot DMA ring, three steps in
+    flight) vs fp32 torch and vs the 128-row register-ring kernel on the same shapes (256- and
+    128-wide column tiles, split counts whose last split is short, accumulation into a sink)."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, C, K = shape
+    x, w = _mk(N, H, H, C, K, 1)
+    wf = w.float().requires_grad_(True)
+    out = F.conv2d(x.float(), wf)
+    dy = torch.randn_like(out).bfloat16()
+    (dw_ref,) = torch.autograd.grad(out, wf, dy.float())
+    dyh, xh = dy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    prev = m.wgrad1x1_big_set(1)
+    try:
+        dw = m.conv_wgrad(dyh, xh, 1, 1, 1, 0, splits, 10)
+        assert _rel(dw.permute(0, 3, 1, 2), dw_ref) < 5e-3
+        sink = torch.full((K, 1, 1, C), 0.25, device=gpu)
+        m.conv_wgrad(dyh, xh, 1, 1, 1, 0, splits, 10, sink, True)
+        assert _rel(sink - 0.25, dw.float()) < 1e-5
+        m.wgrad1x1_big_set(0)
+        dw_old = m.conv_wgrad(dyh, xh, 1, 1, 1, 0, splits, 10)
+        assert _rel(dw, dw_old) < 1e-5
+    finally:
+        m.wgrad1x1_big_set(prev)

@@ -10,5 +10,5 @@ python tools/rocpd_to_csv.py /tmp/pc5 > /dev/null
 d=$(dirname $(find /tmp/pc5 -name "run_kernel_trace.csv" | head -1))
 n=$(grep -c "wprep_kernel" $d/run_kernel_trace.csv)
 echo "steps (wprep launches): $n"
-python tools/rocprof_summary.py $d --steps $n > $O/summary.txt
+python tools/rocprof_summary.py $d --steps $((n - 1)) > $O/summary.txt
 head -40 $O/summary.txt
