@@ -1734,7 +1734,8 @@ void register_conv_bn(pybind11::module& m) {
         "block target of the dedicated 1x1/3x3 wgrad kernels' split heuristic (SDX_W3_BLOCKS); returns the previous value",
         pybind11::arg("n"));
   m.def("wgrad1x1_big_set", [](int64_t on) { return (int64_t)wgrad1x1_big_set((int)on); },
-        "256-row LDS-DMA 1x1 wgrad kernel on (1) / off (0); returns the previous value", pybind11::arg("on"));
+        "256-row LDS-DMA 1x1 wgrad kernel: 0 off, 1 long-split shapes (default), 2 every eligible shape; returns the previous value",
+        pybind11::arg("mode"));
   m.def("tap3_set", &tap3_set,
         "tap-reuse 3x3 conv loop on (1) / off (0) for auto tile selection; returns the previous value",
         pybind11::arg("on"));

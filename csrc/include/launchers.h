@@ -165,8 +165,9 @@ int wgrad1x1_slices(const ConvGeom& g, int splits);
 bool wgrad1x1_pair_view(const ConvGeom& g);
 // runtime switch of the pixel-pair view (tests / A/B); returns the previous value
 int wgrad1x1_pairs_set(int on);
-// the 256-row LDS-DMA kernel on/off (SDX_W1_BIG); returns the previous setting
-int wgrad1x1_big_set(int on);
+// the 256-row LDS-DMA kernel: 0 off, 1 long-split shapes only (default), 2 every eligible
+// shape (SDX_W1_BIG); returns the previous setting
+int wgrad1x1_big_set(int mode);
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s);
 

@@ -81,6 +81,30 @@ __device__ bool xg_exchange(double (&t)[NS], int c, int C, const XgmiCol& xg, in
                            kScope);
     }
   }
+  // Ordering argument (why no system-scope release / acquire fences).
+  //  Producer: every data store above is a system-scope atomic store (sc0 sc1: write-
+  //   through, never held in this GPU's L1/L2) into the destination rank's arena, which is
+  //   allocated uncached (hipDeviceMallocUncached) and, for peers, reached over xGMI. The
+  //   vmcnt(0) below returns only when each store is ACKNOWLEDGED by the memory that owns the
+  //   arena (its memory controller, behind which that GPU's own uncached loads are served),
+  //   i.e. the bytes are globally visible. Only then does the same wave (lanes p < W, after
+  //   the barrier) issue the flag stores, themselves system-scope write-through: a flag can
+  //   never be visible before the data it publishes. A release fence would add nothing for
+  //   these bytes -- its buffer_wbl2 writes back DIRTY L2 lines, and the payload never sits
+  //   in L2 -- but it would write back the whole XCD L2 (the producing conv's output) in
+  //   every exchange: ~2-7 us x 106 exchanges per step.
+  //  Consumer: wave 0 polls its flags with system-scope loads (sc0 sc1: fetched from the
+  //   arena's memory on every poll, never from a cache), waits for the value (the compare
+  //   consumes it), passes the barrier and only THEN issues the data loads, also system-scope
+  //   loads of the uncached arena that bypass L1/L2. No load of the payload can be served from
+  //   a cache line older than the flag, so the acquire's buffer_inv (which would drop the
+  //   XCD's L2) is not needed either.
+  //  Both arguments rest on every payload and flag access being a system-scope atomic on the
+  //   uncached arena (checked: no plain load or store of xg.peers.* exists) and on vmcnt
+  //   acknowledgement meaning completion at the destination for write-through stores, which
+  //   is how CDNA reports them. Same-device IPC (tests/test_gpu_dist.py, 4 processes,
+  //   >300 exchanges) and the emulation exercise the same instruction sequence; a cross-
+  //   device run is the remaining check (the default transport is RCCL until then).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's data stores are acknowledged
   if (threadIdx.x == 0) ok = 1;
   __syncthreads();

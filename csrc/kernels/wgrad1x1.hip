@@ -707,13 +707,30 @@ bool w1_pipe_enabled(const ConvGeom& g);
 std::atomic<int>& w1_big_flag() {
   static std::atomic<int> on{[] {
     const char* e = getenv("SDX_W1_BIG");
-    return e == nullptr || atoi(e) != 0 ? 1 : 0;
+    return e == nullptr ? 1 : atoi(e) < 0 ? 0 : atoi(e) > 2 ? 2 : atoi(e);
   }()};
   return on;
 }
+// SDX_W1_BIG / wgrad1x1_big_set: 0 off, 1 (default) by the rule below, 2 every eligible shape.
+// Only for GEMMs with steps_total x tiles >= SDX_W1_BIG_MIN (default 8192: >= 64 steps per
+// split at the 128-block in-step target). Stand-alone the kernel is 2-12 % faster on every
+// layer 2-4 shape; in the step, on every shape, it made the step 0.04 ms SLOWER (11.786 vs
+// 11.749 ms, 3 interleaved rounds, profiles/w1_big_ab_r6.txt): its 128 KiB of LDS per block
+// leaves no room for a main-stream block on its CU, and at 32 steps per split its fp32 slab
+// round trip (twice the old kernel's at the same block count) eats the gain. The long-split
+// shapes (projection blocks, l2 expand convs) keep 9-12 %.
 bool w1_big(const ConvGeom& g) {
-  return w1_big_flag().load(std::memory_order_relaxed) != 0 && !w1_pairs(g) && g.K % W1B_BM == 0 && g.C % 128 == 0 && w1_pipe_enabled(g) &&
-         (g.stride == 1 || 32 % g.Q == 0);
+  static const long min_work = [] {
+    const char* e = getenv("SDX_W1_BIG_MIN");
+    return e ? atol(e) : 8192L;
+  }();
+  const int mode = w1_big_flag().load(std::memory_order_relaxed);   // 0 off, 1 by the rule, 2 always
+  if (!(mode != 0 && !w1_pairs(g) && g.K % W1B_BM == 0 && g.C % 128 == 0 &&
+        w1_pipe_enabled(g) && (g.stride == 1 || 32 % g.Q == 0)))
+    return false;
+  const long steps = (long)g.N * g.P * g.Q / 32;
+  const long tiles = (long)(g.K / W1B_BM) * (g.C / (g.C % 256 == 0 ? 256 : 128));
+  return mode == 2 || steps * tiles >= min_work;
 }
 
 int wgrad1x1_bn(const ConvGeom& g) {
@@ -767,7 +784,7 @@ bool wgrad1x1_pair_view(const ConvGeom& g) { return w1_pairs(g); }
 
 int wgrad1x1_pairs_set(int on) { return w1_pairs_flag().exchange(on ? 1 : 0); }
 
-int wgrad1x1_big_set(int on) { return w1_big_flag().exchange(on ? 1 : 0); }
+int wgrad1x1_big_set(int mode) { return w1_big_flag().exchange(mode < 0 ? 0 : mode > 2 ? 2 : mode); }
 
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s) {

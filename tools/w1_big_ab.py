@@ -27,14 +27,14 @@ for name, N, H, C, K, st in SHAPES:
     out = torch.empty(K, 1, 1, C, device=dev, dtype=torch.float32)
     row = []
     for big in (0, 1):
-        m.wgrad1x1_big_set(big)
+        m.wgrad1x1_big_set(2 * big)
         t = timeit(lambda: m.conv_wgrad(dy, x, 1, 1, st, 0, 0, -1, out), 20)
         tot[big] += t
         row.append(t)
     fl = 2.0 * N * P * P * C * K
     line = f"{name:8s} old {row[0]:7.1f} us  big {row[1]:7.1f} us  ({fl / row[1] / 1e6:6.1f} TF/s)"
     if sweep:
-        m.wgrad1x1_big_set(1)
+        m.wgrad1x1_big_set(2)
         line += "  splits " + " ".join(
             f"{s}:{timeit(lambda: m.conv_wgrad(dy, x, 1, 1, st, 0, s, 10, out), 20):.1f}" for s in (2, 4, 8, 16, 32, 64))
     print(line, flush=True)
