@@ -1134,6 +1134,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     // LDS (C staging): this wave's drain, then a barrier behind every wave's drain
     vm_wait<0>();
     __syncthreads();
+  } else if constexpr (DEPTH == 3 && ONE) {
+    // single stage: each K-tile is loaded, then computed, in turn (no overlap inside the
+    // block). With a short reduction (SDX_IGEMM_ONE_K) the half-size LDS lets more blocks
+    // share a CU, and their loads overlap each other's MFMAs and epilogues instead
+    for (int kt = 0; kt < nk; ++kt) {
+      issue_glds(k_begin + kt * BK, 0);
+      __syncthreads();
+      if (kt == 0) stamp(1);
+      compute(0);
+      __syncthreads();
+    }
   } else if constexpr (DEPTH == 3) {
     // the DMA of tile k+1 overlaps the MFMAs of tile k; the barrier's vmcnt(0) lands it
     if (nk > 0) issue_glds(k_begin, 0);
@@ -1648,6 +1659,23 @@ int igemm_one() {
   }();
   return v;
 }
+// longest reduction (GEMM K) run on the single-stage DEPTH 3 form: forward
+// SDX_IGEMM_ONE_K (default 256), data gradient SDX_IGEMM_ONE_K_DGRAD (default BK = one
+// K-tile, the only case before round 6). Up to 256 the forward 1x1 GEMMs gain 5-12 % (3
+// blocks per CU instead of 2: l3.x.c3 32.1 -> 29.6 us, l2.x.c3 47.2 -> 42.3, stem 34.2 ->
+// 28.7); the dgrads are mixed (l1.0.c3 61.9 -> 56.4, l3.0.c1 65.0 -> 71.3), and K = 512
+// loses on both (profiles/one_stage_r6.txt)
+int igemm_one_k(int mode) {
+  static const int f = [] {
+    const char* e = getenv("SDX_IGEMM_ONE_K");
+    return e ? atoi(e) : 256;
+  }();
+  static const int d = [] {
+    const char* e = getenv("SDX_IGEMM_ONE_K_DGRAD");
+    return e ? atoi(e) : BK;
+  }();
+  return mode == MODE_FWD ? f : d;
+}
 
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR>
 hipError_t launch_v(bool one, int grid, const IgemmParams& p, hipStream_t s) {
@@ -1669,7 +1697,7 @@ hipError_t launch_k(bool bs, int grid, const IgemmParams& p, hipStream_t s) {
   // LDS-DMA main loops (DEPTH 3: two buffers; 6: in-wave pipelined ring; 7 / 8: tap reuse)
   // carry every epilogue variant; the single-stage (ONE) form is DEPTH 3 at one K-tile
   constexpr bool GLK = (DEPTH == 3 || DEPTH >= 6) && MODE != MODE_WGRAD;
-  const bool one = DEPTH == 3 && p.Kdim <= BK && igemm_one();
+  const bool one = DEPTH == 3 && p.Kdim <= igemm_one_k(MODE) && igemm_one();
   if (MODE == MODE_FWD && p.bn_sc != nullptr) {
     // block-output BN-apply epilogue (forward-folded BN3): LDS-DMA tiles only
     if constexpr (MODE == MODE_FWD && GLK) return launch_v<MODE, BM, BN, WM, WN, DEPTH, 2>(one, grid, p, s);
