@@ -509,10 +509,19 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
 constexpr int W1B_BM = 256;
 constexpr int W1B_NS = 4;   // LDS slots
 
-__device__ __forceinline__ void w1_glds16(w1_gptr src, void* lds) {
-  asm volatile("" : "+v"(src));   // one DMA per select (no duplicated exec-masked branches)
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+// One 16-B LDS-DMA per lane into LDS byte address lds_addr (wave-uniform) + 16·lane, as
+// inline asm: hipcc never learns that it writes LDS, so it does not order the builtin
+// fragment reads behind it (through __builtin_amdgcn_global_load_lds every ds_read of the
+// loop was preceded by an s_waitcnt vmcnt(0) that drained the ring -- it cannot tell that
+// the DMA targets another slot). The reads stay builtins, so hipcc's own lgkmcnt waits
+// guard their uses; the DMAs are ordered for the reads only by the counted vmcnt + barrier
+// of the loop. (Reads in asm instead are unsafe: hipcc may touch an asm output register --
+// a v_bfi re-packing the two halves of a fragment -- while its LDS load is still in flight.)
+__device__ __forceinline__ void w1_glds16(w1_gptr src, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+               : "memory", "m0");
 }
 template <int N>
 __device__ __forceinline__ void w1_vm_wait() {
@@ -569,9 +578,10 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_big_kernel(W1Params p) {
   w1_gptr zp = (w1_gptr)w1_zero16;
   asm volatile("" : "+s"(zp));
   const w1_gptr gdy = (w1_gptr)p.dy, gx = (w1_gptr)p.x;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)smem;
   auto issue = [&](int step) __attribute__((always_inline)) {
     const bool ok = step < s_end;
-    unsigned char* st = smem + (step % W1B_NS) * STAGE;
+    const uint32_t st = lds0 + (uint32_t)((step % W1B_NS) * STAGE);
 #pragma unroll
     for (int i = 0; i < ND_A; ++i)
       w1_glds16(ok ? gdy + (a_src[i] + step * sA) : zp, st + (wv * ND_A + i) * 1024);
@@ -588,25 +598,17 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_big_kernel(W1Params p) {
     const int col = col0 + 4 * pp;
     return w1_off<COLS>(row, col >> 3) + (col & 7) * 2;
   };
-  // LDS byte addresses of stage 0 (a stage adds k % 4 · STAGE)
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)smem;
-  uint32_t ao[TM], bo[TN];
+  // stage-0 byte offsets of the fragments (a stage adds k % 4 · STAGE); pixel row p_hi =
+  // p_lo + 4 is a constant 4·COLS·2 bytes further (the swizzle ignores row bit 2)
+  int ao[TM], bo[TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) ao[i] = lds0 + kout(std::integral_constant<int, W1B_BM>{}, p_lo, wm * 128 + 16 * i);
+  for (int i = 0; i < TM; ++i) ao[i] = kout(std::integral_constant<int, W1B_BM>{}, p_lo, wm * 128 + 16 * i);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bo[j] = lds0 + A_BYTES + kout(std::integral_constant<int, BN>{}, p_lo, wn * WN_COLS + 16 * j);
-  // The transposed fragment reads are inline asm: issued through the builtin, every one of
-  // them is ordered by hipcc behind ALL pending LDS-DMAs (it cannot tell that they target
-  // another slot) -- an s_waitcnt vmcnt(0) at the top of each step that drains the ring. In
-  // asm the compiler neither waits for them, so each use is preceded by a counted lgkmcnt
-  // (LDS returns in order; the loop issues no scalar loads) that also names the fragment as
-  // an operand, pinning the MFMAs behind it. pixel row p_hi = p_lo + 4 is a constant
-  // 4·COLS·2 bytes further (the swizzle ignores row bit 2).
-  auto frag = [&](uint32_t a, auto cols_tag) __attribute__((always_inline)) -> bf16x8 {
+  for (int j = 0; j < TN; ++j) bo[j] = A_BYTES + kout(std::integral_constant<int, BN>{}, p_lo, wn * WN_COLS + 16 * j);
+  auto frag = [&](const unsigned char* b, int o, auto cols_tag) __attribute__((always_inline)) -> bf16x8 {
     constexpr int HI = 4 * decltype(cols_tag)::value * 2;
-    bf16x4 lo, hi;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a), "i"(HI));
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w1_lds_bf16x4*)(b + o));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w1_lds_bf16x4*)(b + o + HI));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
@@ -620,23 +622,18 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_big_kernel(W1Params p) {
   // passes the barrier (its lgkmcnt(0) also completes step k's fragment reads, issued one
   // iteration earlier), issues step k+1's fragment reads and step k+4's DMA into step k's
   // slot (every wave has finished reading it: the barrier), then runs step k's MFMAs on the
-  // fragments in registers -- the reads and the DMA fly under the MFMAs. The fragments are
-  // tied behind the barrier by empty asm so no MFMA is scheduled above its wait.
+  // fragments in registers -- the reads and the DMA fly under the MFMAs.
   auto read_set = [&](int k, bf16x8 (&fa)[TM], bf16x8 (&fb)[TN]) __attribute__((always_inline)) {
-    const uint32_t st = (uint32_t)((k % W1B_NS) * STAGE);
+    const unsigned char* b = smem + (k % W1B_NS) * STAGE;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) fb[j] = frag(bo[j] + st, std::integral_constant<int, BN>{});
+    for (int j = 0; j < TN; ++j) fb[j] = frag(b, bo[j], std::integral_constant<int, BN>{});
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[i] = frag(ao[i] + st, std::integral_constant<int, W1B_BM>{});
+    for (int i = 0; i < TM; ++i) fa[i] = frag(b, ao[i], std::integral_constant<int, W1B_BM>{});
   };
   auto iter = [&](int k, bf16x8 (&ca)[TM], bf16x8 (&cb)[TN], bf16x8 (&na)[TM], bf16x8 (&nb)[TN])
       __attribute__((always_inline)) {
     w1_vm_wait<2 * ND>();
     w1_lds_barrier();
-#pragma unroll
-    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(ca[i]));
-#pragma unroll
-    for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(cb[j]));
     read_set(k + 1, na, nb);
     issue(k + 4);
 #pragma unroll
@@ -656,7 +653,6 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_big_kernel(W1Params p) {
     iter(k, fa0, fb0, fa1, fb1);
     if (k + 1 < s_end) iter(k + 1, fa1, fb1, fa0, fb0);
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the last (unused) fragment reads
   w1_vm_wait<0>();   // the tail DMAs (zero page) land before the block's LDS is released
 
   float* out = p.part + (size_t)split * p.K * p.C;
