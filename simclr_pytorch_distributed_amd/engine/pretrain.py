@@ -524,12 +524,12 @@ class PretrainEngine:
         # The step is captured as ONE chain: the weight gradients run in line on the capture
         # stream instead of forking to the wgrad side stream (SDX_GRAPH_SIDE=1 keeps the
         # fork). A captured two-stream DAG replays its branches on several hardware queues
-        # with no stream priority and a cross-queue wait at every fork: 24.9 vs 11.9 ms
-        # eager at 256 images/GPU, while each kernel replayed on its own runs at its eager
-        # speed (profiles/graph_probe_r6.txt).
+        # with a cross-queue wait at every fork: 24.9 vs 11.9 ms eager at 256 images/GPU
+        # (23.5 ms even with per-node priorities), while each kernel replayed on its own runs
+        # at its eager speed (profiles/graph_probe_r6.txt, profiles/graph_ab_r6.txt).
         # In line, the dedicated wgrad kernels get the whole chip (their eager block target
         # keeps half of it for the concurrent critical path): SDX_GRAPH_WGRAD_BLOCKS, 256.
-        from ..ops import _ext, streams
+        from ..ops import streams
         side_prev = streams.ENABLED
         streams.ENABLED = os.environ.get("SDX_GRAPH_SIDE", "0") == "1"
         m = _ext.require()
