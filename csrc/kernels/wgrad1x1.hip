@@ -502,7 +502,9 @@ __global__ __launch_bounds__(W1_NT, 1) void wgrad1x1_pipe_kernel(W1Params p) {
 //
 // Loop (step k in slot k % 4): see the pipeline note at the loop; three steps' DMAs are in
 // flight under every step's MFMAs.
-// No other vector-memory instruction runs in the loop, so the counted vmcnt is exact, and
+// No other vector-memory instruction runs in the loop, so the counted vmcnt is exact (a
+// compiler spill to scratch would only make it stricter: vmcnt(N) then retires one more of
+// the older DMAs, never fewer), and
 // the barrier is the raw s_barrier (a __syncthreads() would drain the ring, vmcnt(0)).
 // Steps past the split's end DMA the zero page into their (never read) slot, keeping the
 // per-iteration DMA count uniform.
