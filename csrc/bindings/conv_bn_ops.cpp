@@ -1730,6 +1730,9 @@ void register_conv_bn(pybind11::module& m) {
         pybind11::arg("relu"));
   m.def("wgrad1x1_pairs_set", [](int64_t on) { return (int64_t)wgrad1x1_pairs_set((int)on); },
         "pixel-pair 1x1 wgrad for 64-channel sides on (1) / off (0); returns the previous value", pybind11::arg("on"));
+  m.def("igemm_one_k_set", [](int64_t mode, int64_t k) { return (int64_t)igemm_one_k_set((int)mode, (int)k); },
+        "longest GEMM reduction on the single-stage LDS-DMA loop (mode 0 fwd, 1 dgrad); returns the previous limit",
+        pybind11::arg("mode"), pybind11::arg("k"));
   m.def("wgrad_block_target_set", &wgrad_block_target_set,
         "block target of the dedicated 1x1/3x3 wgrad kernels' split heuristic (SDX_W3_BLOCKS); returns the previous value",
         pybind11::arg("n"));

@@ -168,6 +168,9 @@ int wgrad1x1_pairs_set(int on);
 // the 256-row LDS-DMA kernel: 0 off, 1 long-split shapes only (default), 2 every eligible
 // shape (SDX_W1_BIG); returns the previous setting
 int wgrad1x1_big_set(int mode);
+// longest GEMM reduction on the single-stage LDS-DMA loop (mode 0 forward, 1 data gradient;
+// SDX_IGEMM_ONE_K / _DGRAD); returns the previous limit
+int igemm_one_k_set(int mode, int k);
 hipError_t launch_wgrad1x1(const ConvGeom& g, const void* dy, const void* x, float* partial, float* dw, int splits,
                            int accumulate, hipStream_t s);
 

@@ -27,6 +27,8 @@
 // (per-M-tile Σy, Σy² of the stored values → one slab row, reduced in fp64 by
 // bn_stats_reduce). WGRAD writes an fp32 partial slab per K-split (deterministic; reduced
 // by igemm_splitk_reduce), never atomics. Block→tile order is XCD-aware.
+#include <atomic>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -1665,17 +1667,18 @@ int igemm_one() {
 // blocks per CU instead of 2: l3.x.c3 32.1 -> 29.6 us, l2.x.c3 47.2 -> 42.3, stem 34.2 ->
 // 28.7); the dgrads are mixed (l1.0.c3 61.9 -> 56.4, l3.0.c1 65.0 -> 71.3), and K = 512
 // loses on both (profiles/one_stage_r6.txt)
-int igemm_one_k(int mode) {
-  static const int f = [] {
+std::atomic<int>& igemm_one_k_ref(int mode) {
+  static std::atomic<int> f{[] {
     const char* e = getenv("SDX_IGEMM_ONE_K");
     return e ? atoi(e) : 256;
-  }();
-  static const int d = [] {
+  }()};
+  static std::atomic<int> d{[] {
     const char* e = getenv("SDX_IGEMM_ONE_K_DGRAD");
     return e ? atoi(e) : BK;
-  }();
+  }()};
   return mode == MODE_FWD ? f : d;
 }
+int igemm_one_k(int mode) { return igemm_one_k_ref(mode).load(std::memory_order_relaxed); }
 
 template <int MODE, int BM, int BN, int WM, int WN, int DEPTH, int VAR>
 hipError_t launch_v(bool one, int grid, const IgemmParams& p, hipStream_t s) {
@@ -2230,3 +2233,7 @@ hipError_t igemm_trace_copy(unsigned long long* host, hipStream_t s) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_igemm_trace), sizeof(unsigned long long) * 2 * kTraceSlots, 0,
                              hipMemcpyDeviceToHost);
 }
+
+// single-stage reduction limits at run time (tests, A/B): mode 0 forward, 1 data gradient;
+// returns the previous limit
+int igemm_one_k_set(int mode, int k) { return igemm_one_k_ref(mode == 0 ? MODE_FWD : MODE_DGRAD).exchange(k); }

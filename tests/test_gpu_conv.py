@@ -477,3 +477,34 @@ def test_wgrad1x1_big_matches_128row_kernel(gpu, shape, splits):
         assert _rel(dw, dw_old) < 1e-5
     finally:
         m.wgrad1x1_big_set(prev)
+
+
+@pytest.mark.parametrize("mode,shape", [("fwd", (8, 8, 256, 1024)), ("fwd", (16, 16, 128, 512)),
+                                        ("fwd", (4, 8, 200, 256)), ("dgrad", (8, 8, 1024, 256)),
+                                        ("dgrad", (16, 16, 512, 128))])
+def test_single_stage_loop_matches_two_stage(gpu, mode, shape):
+    """The single-stage DEPTH 3 loop over several K-tiles (igemm_one_k_set: forward 1x1 GEMMs
+    with K <= 256 by default) issues the same MFMAs in the same order as the two-stage loop,
+    so outputs and BN statistics are bit-identical; also vs fp32 torch."""
+    from simclr_pytorch_distributed_amd.ops import _ext
+    m = _ext.require()
+    N, H, C, K = shape
+    x, w = _mk(N, H, H, C, K, 1)
+    xh, wh = x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).contiguous()
+    mi = 0 if mode == "fwd" else 1
+    outs = []
+    for lim in (64, 4096):
+        prev = m.igemm_one_k_set(mi, lim)
+        try:
+            if mode == "fwd":
+                outs.append(m.conv_fwd(xh, wh, 1, 0, True, -1))
+            else:
+                dy = torch.randn(N, H, H, K, device=gpu, generator=torch.Generator(gpu).manual_seed(3)).bfloat16()
+                outs.append([m.conv_dgrad(dy, wh.permute(3, 1, 2, 0).contiguous(), H, H, 1, 0, -1)])
+        finally:
+            m.igemm_one_k_set(mi, prev)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    if mode == "fwd":
+        ref = F.conv2d(x.float(), w.float())
+        assert _rel(outs[1][0].permute(0, 3, 1, 2), ref) < 1e-2
