@@ -1079,8 +1079,19 @@ hipEvent_t next_event() {
   static size_t next = 0;
   std::lock_guard<std::mutex> lk(mu);
   if (pool.empty()) {
+    // The pool only orders the two streams of one device (record on one, hipStreamWaitEvent
+    // on the other); the kernels' own dispatch fences publish their writes device-wide. A
+    // record's default system-scope release (L2 writeback + invalidate) is for host / peer
+    // visibility, which nothing here needs: without it the main stream's bubble at each fork
+    // point drops from ~7.0 to ~5.0 us (48 forks per step) and the step by 0.11 ms (3/3
+    // same-box rounds, profiles/event_fence_r6.txt). SDX_EV_FENCE: 0 = the default fence,
+    // 1 = hipEventDisableSystemFence (default), 2 = hipEventReleaseToDevice (-0.03 ms)
+    const char* ef = getenv("SDX_EV_FENCE");
+    const int fm = ef ? atoi(ef) : 1;
+    const unsigned fl = hipEventDisableTiming | (fm == 1 ? hipEventDisableSystemFence : 0u) |
+                        (fm == 2 ? hipEventReleaseToDevice : 0u);
     pool.resize(512);
-    for (auto& e : pool) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    for (auto& e : pool) check_hip(hipEventCreateWithFlags(&e, fl), "hipEventCreate");
   }
   hipEvent_t e = pool[next];
   next = (next + 1) % pool.size();
