@@ -174,7 +174,8 @@ std::vector<torch::Tensor> conv_fwd_impl(torch::Tensor x, torch::Tensor w, int64
   torch::Tensor slab;
   float* sp = nullptr;
   if (want_stats) {
-    const int64_t mt = (M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg);
+    const int64_t mt = g.stride == 1 ? igemm_conv_mtiles(g, g.C, (int)cfg, M)
+                                     : (M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg);
     slab = torch::empty({mt, 2, g.K}, x.options().dtype(at::kFloat));
     sp = slab.data_ptr<float>();
   } else {

@@ -132,6 +132,9 @@ hipError_t launch_conv_dgrad_merged(const ConvGeom& g, const void* dy, const voi
                                     int cfg, hipStream_t s, const void* addend_mask = nullptr,
                                     const BnBwdStat* bstat = nullptr, int addend_sub = 0);
 // M-tiles of one sub-pixel class launch (= its slab rows with a BnBwdStat)
+// statistics-slab rows (M-tiles) of a stride-1 fwd / dgrad conv with reduction channels cdim
+// under tile config cfg (padded-row tap tiles count virtual rows)
+int64_t igemm_conv_mtiles(const ConvGeom& g, int cdim, int cfg, int64_t M);
 int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg);
 int conv_wgrad_splits(const ConvGeom& g, int cfg, int splits);
 // partial: fp32 [splits][K][R*S*C] workspace (unused when splits == 1 and !accumulate)

@@ -156,8 +156,11 @@ struct IgemmParams {
   // (img, hy, hx) is LDS row img·t_is + hy·t_rs + hx (t_rs = W + 2); its 16-B chunk q sits at
   // q ^ ((hx + t_ky·hy) & 7), conflict-free fragment reads for every tap (see tap_halo_kb).
   // t_hp halo pixels = t_nhp 1-KiB LDS-DMA pieces; t_nch channel chunks; the tile's first
-  // image row y0 within image n0.
-  int t_rs, t_is, t_ky, t_hp, t_nhp, t_nch, t_imgs;
+  // image row y0 within image n0. t_rw > 0: padded rows — an image row of W pixels is t_rw
+  // (a power of two) virtual output rows, so a tile of whole rows exists when W does not divide
+  // BM (56x56, 28x28: config 5); the t_rw − W padded rows compute garbage from neighbouring halo
+  // pixels, are zeroed before the epilogue and never stored
+  int t_rs, t_is, t_ky, t_hp, t_nhp, t_nch, t_imgs, t_rw;
 };
 
 // DEPTH 7 / 8 halo buffer size in KiB: the largest window a BM-row tile needs over the
@@ -942,8 +945,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     unsigned char* const junk = smem + NHB * HKB * 1024;
     unsigned char* const bring = junk + 1024;
     const int HW = g.H * g.W;
-    const int nimg0 = m0 / HW;
-    const int y0 = p.t_imgs > 0 ? 0 : (m0 - nimg0 * HW) / g.W;   // t_imgs 0: a band of one image
+    const int RW = p.t_rw > 0 ? p.t_rw : g.W;   // virtual pixels per image row
+    const int HWv = g.H * RW;
+    const int nimg0 = m0 / HWv;
+    const int y0 = p.t_imgs > 0 ? 0 : (m0 - nimg0 * HWv) / RW;   // t_imgs 0: a band of one image
     const int nch = p.t_nch;
     // halo pieces of this wave: piece wvu + NW·i; lane L carries pixel 8·piece + L/8, physical
     // chunk L%8 = logical chunk (L%8) ^ swizzle. Source element (chunk 0) or -1 (zero: pad ring,
@@ -982,8 +987,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
         x = rem - y * g.W;
       } else {
         img = 0;
-        y = ml / g.W;
-        x = ml - y * g.W;
+        y = ml / RW;
+        x = ml - y * RW;
       }
       const int P0 = img * p.t_is + y * p.t_rs + x, F0 = x + p.t_ky * y;
 #pragma unroll
@@ -1200,6 +1205,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
   }
 
   stamp(kTraceSlots - 4);
+  if constexpr (DEPTH == 7 || DEPTH == 8) {
+    if (p.t_rw > 0) {
+      // padded rows (x >= W; m0 is a multiple of t_rw): exact zeros, as the statistics read
+      // the accumulators
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bool pad = ((wm * WTM + 16 * i + c) & (p.t_rw - 1)) >= g.W;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = pad ? 0.f : acc[i][j][r];
+      }
+    }
+  }
   // ---------------------------------- epilogues ----------------------------------
   // acc[i][j][r] = C[m0 + wm*64 + 16i + c][n0 + wn*64 + 16j + 4h + r]
   // (not compiled into the BN-statistics DGRAD variant: its register budget sits at the
@@ -1307,8 +1326,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(
     const int row = (tid + it * NT) / CPR;
     const int m = m0 + row;
     int o = -1, oa = -1;
-    if (m < p.M && my_col < p.Ncol) {
-      int orow = m;
+    bool mok = m < p.M;
+    int mr = m;
+    if ((DEPTH == 7 || DEPTH == 8) && p.t_rw > 0) {
+      // padded-row tile: virtual row -> pixel, or none
+      const int HWv = g.H * p.t_rw;
+      const int n = m / HWv, rem = m - n * HWv;
+      const int yy = rem / p.t_rw, xx = rem - yy * p.t_rw;
+      mok = n < g.N && xx < g.W;
+      mr = (n * g.H + yy) * g.W + xx;
+    }
+    if (mok && my_col < p.Ncol) {
+      int orow = mr;
       if (MODE == MODE_DGRAD && g.stride != 1) {
         const int hw = p.Hc * p.Wc;
         const int n = m / hw, rem = m - n * hw;
@@ -1799,22 +1828,47 @@ hipError_t launch_cfg(IgemmParams p, hipStream_t s) {
 // (W >= 16), 2 rows (W = 8: ky = 0) or 4 rows (W = 4: ky = 4) — conflict-free ds_read_b128
 // lane groups for every tap (checked by brute force over the lane groups of the LDS table in
 // MI355X_MICROARCH.md); other widths are correct, not conflict-free.
+// SDX_TAP_PAD=0: no padded-row tiles (widths that do not divide BM stay on the implicit GEMM)
+bool tap_pad_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SDX_TAP_PAD");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 bool tap_geom(IgemmParams& p, int bm, int depth, int mode) {
   const ConvGeom& g = p.g;
   if (g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || g.P != g.H || g.Q != g.W) return false;
   if (mode == MODE_DGRAD && (p.ncls > 1 || p.ph != 0 || p.pw != 0 || p.nr != 3 || p.ns != 3)) return false;
   const int cdim = mode == MODE_FWD ? g.C : g.K;
   const int HW = g.H * g.W;
-  if (cdim % 64 != 0 || bm % g.W != 0 || !(HW % bm == 0 || bm % HW == 0)) return false;
+  if (cdim % 64 != 0) return false;
+  p.t_rw = 0;
+  int rw = g.W;
+  if (bm % g.W != 0 || !(HW % bm == 0 || bm % HW == 0)) {
+    // padded rows: a band of bm / rw whole image rows of rw = pow2 >= W virtual pixels each
+    // (fragments of 16 virtual pixels stay inside one row: rw >= 16). Single-chunk DEPTH-8
+    // tiles only: 56x56x64 fwd / dgrad 376 / 378 us vs 389 / 427 on the best implicit-GEMM
+    // tile, but the 128-row DEPTH-7 tile at 28x28x128 runs 446 / 419 vs 258 / 266
+    // (profiles/tap_pad_r6.txt, 1024 views)
+    rw = 16;
+    while (rw < g.W) rw <<= 1;
+    if (!tap_pad_enabled() || depth != 8 || bm % rw != 0 || g.H % (bm / rw) != 0) return false;
+    p.t_rw = rw;
+  }
   p.t_rs = g.W + 2;
-  p.t_imgs = bm >= HW ? bm / HW : 0;
-  const int rows = bm >= HW ? g.H : bm / g.W;
+  p.t_imgs = (p.t_rw == 0 && bm >= HW) ? bm / HW : 0;
+  const int rows = p.t_imgs > 0 ? g.H : bm / rw;
   p.t_is = (rows + 2) * p.t_rs;
   p.t_hp = (p.t_imgs > 0 ? p.t_imgs : 1) * p.t_is;
   p.t_nhp = (p.t_hp + 7) / 8;
   p.t_ky = g.W == 4 ? 4 : 0;
   p.t_nch = cdim / 64;
   if (p.t_nhp > tap_halo_kb(bm)) return false;
+  // padded rows: the last row's padded fragments read up to pixel (rows + 1)·t_rs + rw + 1,
+  // still inside the halo buffer
+  if (p.t_rw > 0 && (rows + 1) * p.t_rs + rw + 2 > tap_halo_kb(bm) * 8) return false;
   if (bm == 256 && p.t_ky != 0) return false;   // the BM = 256 loop keeps 3 address variants
   if (depth == 8 && p.t_nch != 1) return false;
   return true;
@@ -1827,7 +1881,8 @@ hipError_t launch_tap(IgemmParams p, hipStream_t s) {
   if (p.in_scale != nullptr) return hipErrorInvalidValue;
   p.ablate = igemm_ablate();
   p.trace = igemm_trace_on();
-  p.m_tiles = (p.M + BM - 1) / BM;
+  // (padded rows: the virtual rows tile exactly — H is a multiple of the band height)
+  p.m_tiles = p.t_rw > 0 ? p.g.N * p.g.H * p.t_rw / BM : (p.M + BM - 1) / BM;
   p.n_tiles = (p.Ncol + BN - 1) / BN;
   const bool bs = MODE == MODE_DGRAD && p.bs.slab != nullptr;
   return launch_k<MODE, BM, BN, WM, WN, DEPTH>(bs, p.m_tiles * p.n_tiles, p, s);
@@ -1887,6 +1942,20 @@ int igemm_tap_cfg(const ConvGeom& g, int cdim, int ncol) {
     if (tap_geom(p, igemm_tile_m(cfg), cfg == 11 ? 8 : 7, MODE_FWD)) return cfg;
   }
   return -1;
+}
+
+// M-tiles (statistics-slab rows) of a stride-1 fwd / dgrad conv of M output rows under cfg: a
+// padded-row tap tile counts its virtual rows
+int64_t igemm_conv_mtiles(const ConvGeom& g, int cdim, int cfg, int64_t M) {
+  const int bm = igemm_tile_m(cfg);
+  if (bm <= 0) return 0;
+  if (cfg >= 11 && cfg <= 13) {
+    IgemmParams p{};
+    p.g = g;
+    p.g.C = cdim;
+    if (tap_geom(p, bm, cfg == 11 ? 8 : 7, MODE_FWD) && p.t_rw > 0) return (int64_t)g.N * g.H * p.t_rw / bm;
+  }
+  return (M + bm - 1) / bm;
 }
 
 namespace {
@@ -1953,6 +2022,7 @@ int conv_dgrad_class_mtiles(const ConvGeom& g, int ph, int pw, int cfg) {
   int r0, nr, s0, ns, Hc, Wc;
   conv_dgrad_class(g, ph, pw, &r0, &nr, &s0, &ns, &Hc, &Wc);
   const int M = g.N * Hc * Wc, bm = igemm_tile_m(cfg);
+  if (g.stride == 1) return (int)igemm_conv_mtiles(g, g.K, cfg, M);   // (a tap tile may pad rows)
   return (M + bm - 1) / bm;
 }
 

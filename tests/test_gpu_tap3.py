@@ -19,20 +19,40 @@ TAP_BM = {11: 256, 12: 256, 13: 128}
 HALO_KB = {256: 50, 128: 36}
 
 
-def tap_ok(cfg, H, W, cdim):
-    """Python mirror of igemm.hip tap_geom (which geometries a tap cfg accepts)."""
+def tap_geom(cfg, H, W, cdim):
+    """Python mirror of igemm.hip tap_geom: None if the tap cfg rejects the geometry, else the
+    virtual row width of a padded-row tile (0: unpadded)."""
     bm = TAP_BM[cfg]
-    if cdim % 64 or bm % W:
-        return False
+    if cdim % 64:
+        return None
     hw = H * W
-    if not (hw % bm == 0 or bm % hw == 0):
-        return False
-    rows = H if bm >= hw else bm // W
-    imgs = bm // hw if bm >= hw else 1
-    hp = imgs * (rows + 2) * (W + 2)
+    rw = 0
+    if bm % W or not (hw % bm == 0 or bm % hw == 0):
+        rw = 16
+        while rw < W:
+            rw *= 2
+        if cfg != 11 or bm % rw or H % (bm // rw):   # padded rows: the DEPTH-8 tile only
+            return None
+    imgs = bm // hw if (rw == 0 and bm >= hw) else 0
+    rows = H if imgs > 0 else bm // (rw or W)
+    hp = max(imgs, 1) * (rows + 2) * (W + 2)
     if math.ceil(hp / 8) > HALO_KB[bm]:
-        return False
-    return cfg != 11 or cdim == 64
+        return None
+    if rw and (rows + 1) * (W + 2) + rw + 2 > HALO_KB[bm] * 8:
+        return None
+    if cfg == 11 and cdim != 64:
+        return None
+    return rw
+
+
+def tap_ok(cfg, H, W, cdim):
+    return tap_geom(cfg, H, W, cdim) is not None
+
+
+def tap_mtiles(cfg, N, H, W, cdim):
+    """statistics-slab rows: a padded-row tile counts its virtual rows"""
+    bm, rw = TAP_BM[cfg], tap_geom(cfg, H, W, cdim)
+    return N * H * rw // bm if rw else (N * H * W + bm - 1) // bm
 
 
 # (N, H=W, C, K)
@@ -45,6 +65,11 @@ SHAPES = [
     (3, 8, 128, 64),
     (3, 4, 512, 512),    # 8 images per 128-row tile, 8 channel chunks (4 halo buffer swaps)
     (5, 4, 64, 128),
+    # padded rows (config 5 at 224x224, cfg 11 only): 56 -> 64-slot rows (bands of 4 rows)
+    (2, 56, 64, 64),
+    (1, 56, 64, 96),
+    (2, 28, 128, 128),
+    (2, 14, 64, 64),     # 16-slot rows do not band 14 rows: rejected
 ]
 
 
@@ -74,7 +99,7 @@ def test_tap3_fwd(gpu, shape, cfg):
         return
     ref = F.conv2d(x.float(), w.float(), padding=1)
     y, slab = m.conv_fwd(xh, wh, 1, 1, True, cfg)
-    assert slab.shape[0] == (N * H * H + TAP_BM[cfg] - 1) // TAP_BM[cfg]
+    assert slab.shape[0] == tap_mtiles(cfg, N, H, H, C)
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
     sums = m.bn_stats_reduce(slab)
     yf = ref.permute(0, 2, 3, 1).reshape(-1, K).double()
@@ -110,7 +135,8 @@ def test_tap3_dgrad(gpu, shape, cfg):
     assert _rel(dx2.float(), dx.float() + add.float()) < 2e-2
 
 
-@pytest.mark.parametrize("shape", [(3, 32, 64, 64), (3, 16, 128, 128), (5, 8, 256, 256), (3, 4, 512, 512)])
+@pytest.mark.parametrize("shape", [(3, 32, 64, 64), (3, 16, 128, 128), (5, 8, 256, 256), (3, 4, 512, 512),
+                                   (2, 56, 64, 64)])
 def test_tap3_dgrad_bnstat(gpu, shape):
     """dgrad + fused BN-backward statistics on the tap-reuse tiles (auto dispatch) against
     the same epilogue on the implicit-GEMM tile (cfg 4): equal statistics up to fp32
@@ -135,20 +161,31 @@ def test_tap3_dgrad_bnstat(gpu, shape):
     assert torch.allclose(s_tap, s_ref, rtol=1e-3, atol=1e-1)
 
 
-@pytest.mark.parametrize("shape", [(4, 32, 64, 64), (4, 16, 128, 128), (8, 8, 256, 256), (16, 4, 512, 512)])
+def _want(H, cdim, ncol):
+    """the tap cfg auto dispatch picks (igemm_tap_cfg candidate order)"""
+    for cfg in ([11] if cdim == 64 and ncol <= 64 else []) + ([12] if H >= 8 else []) + [13]:
+        if tap_ok(cfg, H, H, cdim):
+            return cfg
+    return None
+
+
+@pytest.mark.parametrize("shape", [(4, 32, 64, 64), (4, 16, 128, 128), (8, 8, 256, 256), (16, 4, 512, 512),
+                                   (2, 56, 64, 64)])
 def test_tap3_auto_dispatch(gpu, shape):
-    """auto (cfg -1) runs the tap-reuse loop on every CIFAR ResNet 3x3 stride-1 shape."""
+    """auto (cfg -1) runs the tap-reuse loop on every CIFAR ResNet 3x3 stride-1 shape and on
+    the padded-row 56x56 stage of the 224x224 config."""
     from simclr_pytorch_distributed_amd.ops import _ext
     m = _ext.require()
     N, H, C, K = shape
     x, w = _mk(N, H, C, K, seed=2)
     xh = x.permute(0, 2, 3, 1).contiguous()
     wh = w.permute(0, 2, 3, 1).contiguous()
-    want = 11 if C == 64 and K <= 64 else (12 if H >= 8 else 13)
+    want = _want(H, C, K)
+    assert want is not None
     y_auto, s_auto = m.conv_fwd(xh, wh, 1, 1, True, -1)
     y_tap, s_tap = m.conv_fwd(xh, wh, 1, 1, True, want)
     assert torch.equal(y_auto, y_tap) and torch.equal(s_auto, s_tap)
     dy = torch.randn(N, H, H, K, device="cuda").bfloat16()
     wt = w.permute(1, 2, 3, 0).contiguous()
-    want_d = 11 if K == 64 and C <= 64 else (12 if H >= 8 else 13)
+    want_d = _want(H, K, C)
     assert torch.equal(m.conv_dgrad(dy, wt, H, H, 1, 1, -1), m.conv_dgrad(dy, wt, H, H, 1, 1, want_d))
