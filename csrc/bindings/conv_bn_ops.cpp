@@ -1751,6 +1751,26 @@ void register_conv_bn(pybind11::module& m) {
   m.def("wgrad1x1_big_set", [](int64_t on) { return (int64_t)wgrad1x1_big_set((int)on); },
         "256-row LDS-DMA 1x1 wgrad kernel: 0 off, 1 long-split shapes (default), 2 every eligible shape; returns the previous value",
         pybind11::arg("mode"));
+  m.def("conv_plan", [](int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t R, int64_t S, int64_t stride,
+                        int64_t pad, bool dgrad) {
+    // host-only: the tile config auto dispatch picks for a plain fwd / dgrad and the M-tile
+    // count of its statistics slab (padded-row tap tiles count virtual rows)
+    ConvGeom g{};
+    g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.K = (int)K; g.R = (int)R; g.S = (int)S;
+    g.stride = (int)stride; g.pad = (int)pad;
+    g.P = (g.H + 2 * g.pad - g.R) / g.stride + 1;
+    g.Q = (g.W + 2 * g.pad - g.S) / g.stride + 1;
+    const int64_t M = dgrad ? N * H * W : (int64_t)g.N * g.P * g.Q;
+    const int cdim = dgrad ? g.K : g.C, ncol = dgrad ? g.C : g.K;
+    const int cfg = dgrad ? conv_cfg(g, cdim, ncol, M, (int64_t)R * S * K / (stride * stride), true, true)
+                          : conv_cfg(g, cdim, ncol, M, (int64_t)R * S * C, true, false);
+    const int64_t mt = dgrad ? (g.stride == 1 ? conv_dgrad_class_mtiles(g, 0, 0, cfg) : -1)
+                             : (g.stride == 1 ? igemm_conv_mtiles(g, g.C, cfg, M)
+                                              : (M + igemm_tile_m(cfg) - 1) / igemm_tile_m(cfg));
+    return pybind11::make_tuple(cfg, mt);
+  }, "host-only dispatch plan of a plain conv: (tile config, statistics-slab M-tiles; -1 for strided dgrads)",
+        pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("K"),
+        pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("dgrad"));
   m.def("tap3_set", &tap3_set,
         "tap-reuse 3x3 conv loop on (1) / off (0) for auto tile selection; returns the previous value",
         pybind11::arg("on"));
