@@ -22,6 +22,7 @@ notified through :mod:`ops.sinks`.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import List, Optional
 
@@ -31,6 +32,8 @@ import torch.distributed as dist
 from . import _ext, sinks
 from ..parallel import comm
 from .streams import SideWork
+
+_STEM_SIDE = os.environ.get("SDX_STEM_SIDE", "0") == "1"
 
 
 # off by default: with LDS-DMA staged convs, materialising relu(bn(y)) once is faster than
@@ -281,7 +284,10 @@ class _Stem(torch.autograd.Function):
         w = ctx.enc.conv1.weight
         K, C, R, S = w.shape
         g = sinks.target(w)
-        with SideWork(dy, x):
+        # the stem's weight gradient is the last work of the backward: on the compute stream
+        # (idle from here on) it overlaps the wgrad stream's remaining queue instead of
+        # waiting behind it (SDX_STEM_SIDE=1: on the side stream)
+        with (SideWork(dy, x) if _STEM_SIDE else contextlib.nullcontext()):
             dwk = m.conv_wgrad(dy, x, R, S, st, pad, 0, -1)      # [K][R][S][Cp] fp32
             gk = g.permute(0, 2, 3, 1)                             # [K][R][S][C] (channels_last sink)
             if gk.is_contiguous():
