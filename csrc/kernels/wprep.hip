@@ -17,23 +17,33 @@ struct WSeg {
   long dst_k;    // element offset of Wk in the bf16 output (fwd layout)
   long dst_t;    // element offset of Wt in the bf16 output (dgrad layout), -1: none
   int K, RS, C, Cp;
-  long n;        // K*RS*Cp (fwd elements; the work index space of this segment)
-  long start;    // prefix sum of n
+  long n;        // K*RS*Cp (fwd elements of this segment)
+  long start;    // first tile of this segment: prefix sum of ceil(K/64)·ceil(Cp/64)·RS
 };
 
-// blockIdx.y = conv (segment); blockIdx.x = 64(k) x 64(c) tile at one filter tap rs.
+// One block per 64(k) x 64(c) tile at one filter tap rs, over ALL segments: block b belongs to
+// the last segment whose first tile is <= b (binary search over the uniform segment table).
+// A [largest conv's tiles] x [segments] grid launched ~57k blocks for ~7k tiles of work
+// (the head's 2048x2048 Linear sets the largest); the empty ones cost dispatch time.
 // Reads of the fp32 master and writes of Wk are coalesced along c; the transposed Wt tile
 // goes through LDS so its writes are coalesced along k. Segments with C % 4 == 0 and no
 // channel padding (every conv but the stem, and the head's Linear layers) move 16-B float4
 // loads and 8-B bf16x4 stores per thread (a scalar fp32 load / 2-B store per element made
 // this a latency-bound 72 us pass per step).
 __global__ __launch_bounds__(256) void wprep_kernel(const float* __restrict__ master, uint16_t* __restrict__ out,
-                                                    const WSeg* __restrict__ segs) {
+                                                    const WSeg* __restrict__ segs, int nseg) {
   __shared__ uint16_t tile[64][66];
-  const WSeg s = segs[blockIdx.y];
+  const long b = blockIdx.x;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].start <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const WSeg s = segs[lo];
   const int kt = (s.K + 63) / 64, ct = (s.Cp + 63) / 64;
-  int t = blockIdx.x;
-  if (t >= kt * ct * s.RS) return;
+  int t = (int)(b - s.start);
+  if (t < 0 || t >= kt * ct * s.RS) return;
   const int cti = t % ct; t /= ct;
   const int rs = t % s.RS;
   const int kti = t / s.RS;
@@ -115,10 +125,11 @@ hipError_t launch_unpad_add(const float* src, float* dst, int rows, int Cp, int 
 }
 
 hipError_t launch_wprep(const float* master, void* out, const void* segs, int nseg, long total, hipStream_t s) {
-  // `total` = the largest conv's tile count (ceil(K/64)·ceil(Cp/64)·R·S), computed by the host
-  if (total < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wprep_kernel, dim3((unsigned)total, nseg), dim3(256), 0, s, master, (uint16_t*)out,
-                     (const WSeg*)segs);
+  // `total` = the tile count of all segments (Σ ceil(K/64)·ceil(Cp/64)·R·S); segs[i].start =
+  // the prefix of it (host-computed, ops/weights.py)
+  if (total < 1 || nseg < 1 || total > (1L << 31) - 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wprep_kernel, dim3((unsigned)total), dim3(256), 0, s, master, (uint16_t*)out,
+                     (const WSeg*)segs, nseg);
   SDX_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -29,7 +29,7 @@ class ConvWeightCache:
         self.entries = {}
         rows = []
         off = 0
-        start = 0
+        tile0 = 0                             # first 64x64-tap tile of the next conv (wprep grid)
         ok = master is not None
         for cv in convs:
             w = cv.weight
@@ -50,11 +50,9 @@ class ConvWeightCache:
                     src = (w.data_ptr() - master.data_ptr()) // 4
                     if src < 0 or src + w.numel() > master.numel():
                         ok = False
-                    rows.append([src, e["off_k"], e["off_t"], K | ((R * S) << 32), C | (Cp << 32), n_k, start])
-                    start += n_k
-                    tiles = ((K + 63) // 64) * ((Cp + 63) // 64) * R * S
-                    self.max_tiles = max(getattr(self, "max_tiles", 0), tiles)
-        self.total = start
+                    rows.append([src, e["off_k"], e["off_t"], K | ((R * S) << 32), C | (Cp << 32), n_k, tile0])
+                    tile0 += ((K + 63) // 64) * ((Cp + 63) // 64) * R * S
+        self.tiles = tile0                    # wprep launches one block per tile
         self.buf = torch.empty(off, dtype=torch.bfloat16, device=dev)
         self.native = ok and dev.type == "cuda" and _ext.available()
         self.segs = torch.tensor(rows, dtype=torch.int64, device=dev) if self.native else None
@@ -74,7 +72,7 @@ class ConvWeightCache:
         s = streams.side(dev)
         s.wait_stream(main)
         with torch.cuda.stream(s):
-            _ext.require().wprep(self.master, self.buf, self.segs, self.max_tiles)
+            _ext.require().wprep(self.master, self.buf, self.segs, self.tiles)
         if getattr(self, "_ev", None) is None:
             self._ev = torch.cuda.Event()
         self._ev.record(s)
@@ -88,7 +86,7 @@ class ConvWeightCache:
             self._pending = None
             return
         if self.native:
-            _ext.require().wprep(self.master, self.buf, self.segs, self.max_tiles)
+            _ext.require().wprep(self.master, self.buf, self.segs, self.tiles)
         else:
             for cv in self.convs:
                 e = self.entries[id(cv)]
