@@ -140,8 +140,9 @@ def main():
             torch.cuda.synchronize()
         comm.barrier()
 
-    # --syncbn_comm auto (default) at N > 1: every candidate SyncBN transport is timed on real
-    # steps (state restored afterwards), ranks agree on the fastest; reported in the JSON line
+    # N > 1: the SyncBN transport candidates of --syncbn_comm (default rccl: RCCL only; auto: the
+    # fused xGMI exchange too) are timed on real steps (state restored afterwards), the ranks
+    # agree on the fastest; reported in the JSON line with a local-BN baseline
     tune = eng.autotune_syncbn(next_idx(0), steps=3, baseline=True) if n > 1 and not a.no_syncbn else None
     graphed = False
     if a.graph:
