@@ -53,6 +53,7 @@ class ConvWeightCache:
                     rows.append([src, e["off_k"], e["off_t"], K | ((R * S) << 32), C | (Cp << 32), n_k, tile0])
                     tile0 += ((K + 63) // 64) * ((Cp + 63) // 64) * R * S
         self.tiles = tile0                    # wprep launches one block per tile
+        self.seg_rows = rows                  # [src, off_k, off_t, K|RS<<32, C|Cp<<32, n_k, first tile]
         self.buf = torch.empty(off, dtype=torch.bfloat16, device=dev)
         self.native = ok and dev.type == "cuda" and _ext.available()
         self.segs = torch.tensor(rows, dtype=torch.int64, device=dev) if self.native else None
