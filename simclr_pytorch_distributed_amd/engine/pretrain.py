@@ -38,6 +38,8 @@ from ..ops import _ext
 from ..optim.flat import FlatParams, FusedSGD, build_optimizer
 from ..optim.schedules import adjust_learning_rate, warmup_learning_rate
 from ..parallel import comm
+
+_ZERO_SIDE = os.environ.get("SDX_ZERO_SIDE", "1") != "0"
 from ..parallel.ddp import GradBucketReducer
 from ..utils.logging import setup_logging
 from ..utils.meters import AverageMeter
@@ -400,6 +402,7 @@ class PretrainEngine:
             prefetch = getattr(self.runner, "prefetch_weights", None)
             if prefetch is not None:
                 prefetch()          # weight conversion overlaps the augmentation launch
+            zeroed = self._zero_grad_side()
             x = self.make_views(idx, epoch, it)
             # (SimCLR ignores labels: no gather kernel in its step)
             labels = self.labels[idx] if opt.method == "SupCon" else None
@@ -412,7 +415,10 @@ class PretrainEngine:
             if extra is not None:
                 loss = loss + extra
         with ph("backward"):
-            self.optimizer.zero_grad()
+            if zeroed is not None:
+                torch.cuda.current_stream(self.device).wait_event(zeroed)
+            else:
+                self.optimizer.zero_grad()
             # a persistent seed gradient: no ones-fill kernel per step
             one = getattr(self, "_one_grad", None)
             if one is None or one.device != loss.device or one.dtype != loss.dtype:
@@ -425,6 +431,26 @@ class PretrainEngine:
             self.optimizer.step()
         stats["loss_local"] = loss.detach()
         return stats
+
+    def _zero_grad_side(self):
+        """Zero the gradient buffer on the wgrad side stream at the start of the step (after
+        the previous optimizer update), where it overlaps the forward instead of sitting on
+        the compute stream before the backward (SDX_ZERO_SIDE=0: there). Returns the event
+        the backward waits on, or None when it is left to the backward. The side stream's
+        weight gradients are queued behind it anyway (FIFO)."""
+        from ..ops import streams
+        if not (_ZERO_SIDE and streams.ENABLED and self.device.type == "cuda"):
+            return None
+        main = torch.cuda.current_stream(self.device)
+        s = streams.side(self.device)
+        s.wait_stream(main)
+        with torch.cuda.stream(s):
+            self.optimizer.zero_grad()
+        ev = getattr(self, "_zg_ev", None)
+        if ev is None:
+            ev = self._zg_ev = torch.cuda.Event()
+        ev.record(s)
+        return ev
 
     def _step_body_gradcache(self, idx: torch.Tensor, epoch: int, it: int, mb: int):
         """Gradient-cache step for contrastive batches larger than one encoder pass fits in
