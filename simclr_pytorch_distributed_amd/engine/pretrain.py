@@ -17,6 +17,7 @@ device and are synchronised only every ``print_freq`` steps.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import math
 import os
@@ -40,6 +41,7 @@ from ..optim.schedules import adjust_learning_rate, warmup_learning_rate
 from ..parallel import comm
 
 _ZERO_SIDE = os.environ.get("SDX_ZERO_SIDE", "1") != "0"
+_NORM_SIDE = os.environ.get("SDX_NORM_SIDE", "1") != "0"
 from ..parallel.ddp import GradBucketReducer
 from ..utils.logging import setup_logging
 from ..utils.meters import AverageMeter
@@ -624,6 +626,7 @@ class PretrainEngine:
         (csrc/kernels/featnorm.hip) computes them and advances the record_norm_mean EMA.
         Same semantics as the torch path: global sums are estimated as local·W (no
         collective) when no regulariser needs the exact global statistics."""
+        from ..ops.streams import SideWork
         m = _ext.require()
         x = feats.detach().float().contiguous()
         n_global = float(x.shape[0] * self.world)
@@ -631,12 +634,15 @@ class PretrainEngine:
         sums = getattr(self, "_ns_sums", None)
         if sums is None or sums.device != x.device:
             sums = self._ns_sums = torch.zeros(2, dtype=torch.float64, device=x.device)
-        if self.world > 1:
-            m.norm_stats(x, 0, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
-            sums.mul_(float(self.world))
-            out = m.norm_stats(x, 2, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
-        else:
-            out = m.norm_stats(x, 1, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
+        # nothing in the step reads these: on the wgrad side stream (idle here), off the loss
+        # -> backward path; the end-of-backward join orders every later reader behind them
+        with (SideWork(x) if _NORM_SIDE else contextlib.nullcontext()):
+            if self.world > 1:
+                m.norm_stats(x, 0, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
+                sums.mul_(float(self.world))
+                out = m.norm_stats(x, 2, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
+            else:
+                out = m.norm_stats(x, 1, sums, n_global, mom, self.record_norm_mean, self._rnm_valid)
         return {"extra_loss": None, "norm_mean": out[0], "norm_var": out[1], "loss_sec": out[3],
                 "loss_l2reg": out[4], "record_norm_mean": out[2]}
 
