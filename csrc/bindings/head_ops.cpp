@@ -20,6 +20,7 @@
 #include "ops_decl.h"
 
 #include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
 
 #include <map>
 #include <mutex>
@@ -28,6 +29,8 @@
 hipError_t launch_cast_f32_bf16(const float* x, void* y, long n, hipStream_t s);
 
 namespace sdx_bind {
+std::vector<torch::Tensor>& side_stash();   // conv_bn_ops.cpp: released at the side-stream join
+
 namespace {
 
 void check_w(const torch::Tensor& w, int64_t rows, int64_t cols, const char* name) {
@@ -150,6 +153,29 @@ torch::Tensor gemm_dgrad(const torch::Tensor& dy, const torch::Tensor& wt, int64
   return dx;
 }
 
+// the head's side-stream fork: everything queued on the compute stream so far, then `keep`
+// stays alive until the side stream is joined (side_stash). Own small event pool: two forks
+// per step; no system-scope fence (same-device stream ordering, conv_bn_ops.cpp next_event)
+void head_fork(hipStream_t main, hipStream_t ss, std::initializer_list<torch::Tensor> keep) {
+  static std::mutex mu;
+  static std::vector<hipEvent_t> pool;
+  static size_t next = 0;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (pool.empty()) {
+      pool.resize(64);
+      for (auto& e : pool)
+        check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate");
+    }
+    ev = pool[next];
+    next = (next + 1) % pool.size();
+  }
+  check_hip(hipEventRecord(ev, main), "hipEventRecord");
+  check_hip(hipStreamWaitEvent(ss, ev, 0), "hipStreamWaitEvent");
+  for (const auto& t : keep) side_stash().push_back(t);
+}
+
 // feat [N][D] fp32|bf16; w1 [O1][D] bf16 (+ b1 fp32); MLP: w2 [O2][O1] bf16 (+ b2).
 // Returns [z fp32 [N][O_last], fb bf16 [N][D], h bf16 [N][O1] (MLP; empty otherwise)].
 std::vector<torch::Tensor> head_fwd(torch::Tensor feat, torch::Tensor w1, torch::Tensor b1, OptT w2, OptT b2) {
@@ -170,8 +196,10 @@ std::vector<torch::Tensor> head_fwd(torch::Tensor feat, torch::Tensor w1, torch:
 
 // dz [N][O_last] fp32; w1t [D][O1] / w2t [O1][O2] bf16 (dgrad layouts, Wᵀ); sinks fp32.
 // Accumulates every parameter gradient into its sink; returns dfeat fp32 [N][D].
+// side (a stream handle, 0 = none): the weight gradients and the output bias gradient run
+// on the wgrad side stream, off the data-gradient chain into the encoder's backward
 torch::Tensor head_bwd(torch::Tensor dz, torch::Tensor fb, OptT h, torch::Tensor w1t, OptT w2t, torch::Tensor sw1,
-                       torch::Tensor sb1, OptT sw2, OptT sb2) {
+                       torch::Tensor sb1, OptT sw2, OptT sb2, int64_t side) {
   dz = dz.contiguous();
   check_2d(dz, at::kFloat, "dz");
   check_2d(fb, at::kBFloat16, "fb");
@@ -181,6 +209,26 @@ torch::Tensor head_bwd(torch::Tensor dz, torch::Tensor fb, OptT h, torch::Tensor
   auto dzb = to_bf16(dz);
   const bool mlp = w2t.has_value();
   torch::Tensor& sb_last = mlp ? *sb2 : sb1;
+  if (side != 0 && mlp) {
+    TORCH_CHECK(h.has_value() && sw2.has_value() && sb2.has_value(), "MLP head: h, sw2, sb2 required");
+    check_2d(*h, at::kBFloat16, "h");
+    const int64_t O1 = h->size(1);
+    hipStream_t main = cur_stream(), ss = reinterpret_cast<hipStream_t>(side);
+    auto hs = c10::hip::getStreamFromExternal(ss, dz.device().index());
+    head_fork(main, ss, {dz, dzb, *h});
+    {
+      c10::hip::HIPStreamGuard guard(hs);
+      colsum_into(dz, rows, 1, O, sb_last);
+      gemm_wgrad(dzb, *h, *sw2);
+    }
+    auto dh = gemm_dgrad(dzb, *w2t, O1, false, &*h, &sb1);
+    head_fork(main, ss, {dh, fb});
+    {
+      c10::hip::HIPStreamGuard guard(hs);
+      gemm_wgrad(dh, fb, sw1);
+    }
+    return gemm_dgrad(dh, w1t, D, true, nullptr, nullptr);
+  }
   colsum_into(dz, rows, 1, O, sb_last);   // db_last += Σ_rows dz (dz viewed as a [rows][1][O] slab)
   if (!mlp) {
     gemm_wgrad(dzb, fb, sw1);
@@ -204,7 +252,7 @@ void register_head(pybind11::module& m) {
   m.def("head_bwd", &head_bwd, "projection head backward: gradients into the sinks, returns dfeat fp32",
         pybind11::arg("dz"), pybind11::arg("fb"), pybind11::arg("h"), pybind11::arg("w1t"), pybind11::arg("w2t"),
         pybind11::arg("sw1"), pybind11::arg("sb1"), pybind11::arg("sw2") = pybind11::none(),
-        pybind11::arg("sb2") = pybind11::none());
+        pybind11::arg("sb2") = pybind11::none(), pybind11::arg("side") = 0);
 }
 
 }  // namespace sdx_bind

@@ -13,9 +13,22 @@ output — the reference computed under autocast, with the bias added before rou
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ext, sinks
+
+
+_HEAD_SIDE = os.environ.get("SDX_HEAD_SIDE", "1") != "0"
+
+
+def _side(t: torch.Tensor) -> int:
+    """the wgrad side stream's handle for the head's weight gradients (0: none)"""
+    from . import streams
+    if not (_HEAD_SIDE and streams.ENABLED and t.is_cuda):
+        return 0
+    return streams.side(t.device).cuda_stream
 
 
 class _MLPHead(torch.autograd.Function):
@@ -34,7 +47,7 @@ class _MLPHead(torch.autograd.Function):
         l1, l2 = ctx.mods
         t = sinks.target
         dfeat = _ext.require().head_bwd(dz.float(), fb, h, w1t, w2t, t(l1.weight), t(l1.bias), t(l2.weight),
-                                        t(l2.bias))
+                                        t(l2.bias), _side(dz))
         sinks.notify(ctx.params)
         return (dfeat.to(ctx.feat_dtype), None, None, None, None, None, None) + (None,) * len(ctx.params)
 
