@@ -118,8 +118,9 @@ void gemm_wgrad(const torch::Tensor& dy, const torch::Tensor& x, torch::Tensor& 
 
 // dx[rows][in] = dy[rows][out] · Wt[in][out]ᵀ, optionally ReLU-masked by (ref > 0) with the
 // masked column sums added into `bias_sink` (the hidden layer's bias gradient)
+// (slab_out: the caller reduces the bias-gradient slab itself, e.g. on another stream)
 torch::Tensor gemm_dgrad(const torch::Tensor& dy, const torch::Tensor& wt, int64_t in, bool out_f32,
-                         const torch::Tensor* relu_ref, torch::Tensor* bias_sink) {
+                         const torch::Tensor* relu_ref, torch::Tensor* bias_sink, torch::Tensor* slab_out = nullptr) {
   const int64_t rows = dy.size(0), out = dy.size(1);
   check_w(wt, in, out, "Wt");
   TORCH_CHECK(in % 8 == 0, "input features must be a multiple of 8");
@@ -149,7 +150,8 @@ torch::Tensor gemm_dgrad(const torch::Tensor& dy, const torch::Tensor& wt, int64
   check_hip(launch_conv_dgrad_class(g, 0, 0, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), nullptr, cfg, cur_stream(),
                                     nullptr, &bs, 0, &epi),
             "head gemm_dgrad(relu)");
-  colsum_into(slab, mt, 2, in, *bias_sink);
+  if (slab_out != nullptr) *slab_out = slab;
+  else colsum_into(slab, mt, 2, in, *bias_sink);
   return dx;
 }
 
@@ -221,10 +223,12 @@ torch::Tensor head_bwd(torch::Tensor dz, torch::Tensor fb, OptT h, torch::Tensor
       colsum_into(dz, rows, 1, O, sb_last);
       gemm_wgrad(dzb, *h, *sw2);
     }
-    auto dh = gemm_dgrad(dzb, *w2t, O1, false, &*h, &sb1);
-    head_fork(main, ss, {dh, fb});
+    torch::Tensor slab1;   // the hidden bias gradient's column sums, reduced on the side stream
+    auto dh = gemm_dgrad(dzb, *w2t, O1, false, &*h, &sb1, &slab1);
+    head_fork(main, ss, {dh, fb, slab1});
     {
       c10::hip::HIPStreamGuard guard(hs);
+      colsum_into(slab1, slab1.size(0), 2, O1, sb1);
       gemm_wgrad(dh, fb, sw1);
     }
     return gemm_dgrad(dh, w1t, D, true, nullptr, nullptr);

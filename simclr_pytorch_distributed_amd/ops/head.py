@@ -24,11 +24,22 @@ _HEAD_SIDE = os.environ.get("SDX_HEAD_SIDE", "1") != "0"
 
 
 def _side(t: torch.Tensor) -> int:
-    """the wgrad side stream's handle for the head's weight gradients (0: none)"""
+    """the wgrad side stream's handle for the head's weight gradients (0: none). The current
+    backward pass then ends with a join (compute stream behind the side stream), so the
+    parameter gradients are complete for whatever runs after ``backward()`` on the compute
+    stream, not only for the optimizer step (which joins as well)."""
     from . import streams
     if not (_HEAD_SIDE and streams.ENABLED and t.is_cuda):
         return 0
-    return streams.side(t.device).cuda_stream
+    dev = t.device
+    main, side = torch.cuda.current_stream(dev), streams.side(dev)   # (this node's stream)
+
+    def _join():
+        main.wait_stream(side)
+        streams.release()
+
+    torch.autograd.Variable._execution_engine.queue_callback(_join)
+    return side.cuda_stream
 
 
 class _MLPHead(torch.autograd.Function):
